@@ -1,0 +1,68 @@
+"""ctypes binding of the C ABI in include/hbbft_hip.h (libhbbft_hip.so, built in-tree).
+
+Loading fails loudly when the shared library is missing: there is no CPU fallback anywhere in
+the product path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhbbft_hip.so")
+
+G1_BYTES = 96
+G2_BYTES = 192
+FR_BYTES = 32
+
+# (name, restype, argtypes) for every symbol declared in include/hbbft_hip.h
+_c = ctypes
+_P = _c.c_void_p
+_SZ = _c.c_size_t
+_I = _c.c_int
+SIGNATURES = [
+    ("hbh_engine_create", _I, [_I, _c.POINTER(_P)]),
+    ("hbh_engine_destroy", _I, [_P]),
+    ("hbh_last_error", _c.c_char_p, []),
+    ("hbh_device_count", _I, [_c.POINTER(_I)]),
+    ("hbh_verify_pairing_eq", _I, [_P, _SZ, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _P]),
+    ("hbh_verify_sig_shares", _I, [_P, _SZ, _P, _P, _P, _SZ, _P, _P]),
+    ("hbh_verify_dec_shares", _I, [_P, _SZ, _P, _P, _P, _P, _SZ, _P, _P]),
+    ("hbh_verify_ciphertexts", _I, [_P, _SZ, _P, _P, _P, _P]),
+    ("hbh_verify_pairing_eq_dev", _I, [_P, _P, _SZ, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _P]),
+    ("hbh_dbg_pairing", _I, [_P, _SZ, _P, _P, _P]),
+]
+
+_lib = None
+
+
+class HbhError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libhbbft_hip.so (raises if absent - no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HbhError("libhbbft_hip.so not built (run __graft_entry__.build() or `make -C hbbft_amd`)")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise HbhError("hbbft_hip error %d: %s" % (rc, lib().hbh_last_error().decode()))
+
+
+def buf(b):
+    """bytes-like -> (ctypes buffer, pointer) kept alive by the caller."""
+    if b is None:
+        return None, None
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        cb = (ctypes.c_uint8 * len(b)).from_buffer_copy(bytes(b))
+        return cb, ctypes.cast(cb, ctypes.c_void_p)
+    raise TypeError(type(b))

@@ -1,0 +1,161 @@
+"""Host-side handle on one GPU's batch engine (C ABI in include/hbbft_hip.h).
+
+Inputs are in the ABI point format (affine, canonical little-endian; infinity = all-zero); the
+``wire`` helpers convert from the reference's uncompressed wire encoding (pairing 0.14
+``into_uncompressed``: big-endian, G2 as x.c1 || x.c0 || y.c1 || y.c0, 0x40 flag = infinity).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import G1_BYTES, G2_BYTES, buf, check
+
+
+def _u32(idx, n):
+    if idx is None:
+        return None, None
+    a = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32))
+    if a.shape != (n,):
+        raise ValueError("index array must have shape (n,)")
+    return a, a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _join(points, size):
+    if isinstance(points, (bytes, bytearray)):
+        b = bytes(points)
+    else:
+        b = b"".join(bytes(p) for p in points)
+    if len(b) % size:
+        raise ValueError("point buffer length %d is not a multiple of %d" % (len(b), size))
+    return b
+
+
+class Engine:
+    """One engine per GPU (one process per GPU for multi-GPU runs)."""
+
+    def __init__(self, device=0):
+        self._l = _lib.lib()
+        h = ctypes.c_void_p()
+        check(self._l.hbh_engine_create(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._l.hbh_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ------------------------------------------------------------ pairing-equality checks
+    def verify_pairing_eq(self, p1, q1_table, q1_idx, p2, q2_table, q2_idx):
+        """verdict[i] = e(p1[i], q1[q1_idx[i]]) == e(p2[i], q2[q2_idx[i]])."""
+        p1b, p2b = _join(p1, G1_BYTES), _join(p2, G1_BYTES)
+        q1b, q2b = _join(q1_table, G2_BYTES), _join(q2_table, G2_BYTES)
+        n = len(p1b) // G1_BYTES
+        if len(p2b) // G1_BYTES != n:
+            raise ValueError("p1/p2 length mismatch")
+        nq1, nq2 = len(q1b) // G2_BYTES, len(q2b) // G2_BYTES
+        i1, pi1 = _u32(q1_idx, n)
+        i2, pi2 = _u32(q2_idx, n)
+        out = (ctypes.c_uint8 * max(n, 1))()
+        keep = [buf(x) for x in (p1b, q1b, p2b, q2b)]
+        check(self._l.hbh_verify_pairing_eq(self._h, n, keep[0][1], keep[1][1], nq1, pi1,
+                                            keep[2][1], keep[3][1], nq2, pi2, ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)[:n]
+
+    def verify_sig_shares(self, pks, sigs, hashes, doc_idx):
+        """PublicKeyShare::verify_g2 batch (src/threshold_sign.rs:216-225)."""
+        pkb, sgb, hb = _join(pks, G1_BYTES), _join(sigs, G2_BYTES), _join(hashes, G2_BYTES)
+        n = len(pkb) // G1_BYTES
+        if len(sgb) // G2_BYTES != n:
+            raise ValueError("pks/sigs length mismatch")
+        di, pdi = _u32(doc_idx, n)
+        out = (ctypes.c_uint8 * max(n, 1))()
+        keep = [buf(x) for x in (pkb, sgb, hb)]
+        check(self._l.hbh_verify_sig_shares(self._h, n, keep[0][1], keep[1][1], keep[2][1], len(hb) // G2_BYTES,
+                                            pdi, ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)[:n]
+
+    def verify_dec_shares(self, shares, pks, huv, w, ct_idx):
+        """PublicKeyShare::verify_decryption_share batch (src/threshold_decrypt.rs:220-229)."""
+        sb, pkb = _join(shares, G1_BYTES), _join(pks, G1_BYTES)
+        hb, wb = _join(huv, G2_BYTES), _join(w, G2_BYTES)
+        n = len(sb) // G1_BYTES
+        ci, pci = _u32(ct_idx, n)
+        out = (ctypes.c_uint8 * max(n, 1))()
+        keep = [buf(x) for x in (sb, pkb, hb, wb)]
+        check(self._l.hbh_verify_dec_shares(self._h, n, keep[0][1], keep[1][1], keep[2][1], keep[3][1],
+                                            len(hb) // G2_BYTES, pci, ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)[:n]
+
+    def verify_ciphertexts(self, u, w, huv):
+        """Ciphertext::verify batch (src/threshold_decrypt.rs:142)."""
+        ub, wb, hb = _join(u, G1_BYTES), _join(w, G2_BYTES), _join(huv, G2_BYTES)
+        n = len(ub) // G1_BYTES
+        out = (ctypes.c_uint8 * max(n, 1))()
+        keep = [buf(x) for x in (ub, wb, hb)]
+        check(self._l.hbh_verify_ciphertexts(self._h, n, keep[0][1], keep[1][1], keep[2][1],
+                                             ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)[:n]
+
+    def verify_pairing_eq_dev(self, stream, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, d_v):
+        """Device-pointer variant (ints are raw device addresses, e.g. torch ``data_ptr()``)."""
+        vp = ctypes.c_void_p
+        check(self._l.hbh_verify_pairing_eq_dev(self._h, vp(stream) if stream else None, n, vp(d_p1), vp(d_q1), nq1,
+                                                vp(d_i1) if d_i1 else None, vp(d_p2), vp(d_q2), nq2,
+                                                vp(d_i2) if d_i2 else None, vp(d_v)))
+
+    def dbg_pairing(self, p, q):
+        """e(p[i], q[i])^3 as 12 canonical Fp coefficients (LE, 48 B each) per item."""
+        pb, qb = _join(p, G1_BYTES), _join(q, G2_BYTES)
+        n = len(pb) // G1_BYTES
+        out = (ctypes.c_uint8 * max(n * 576, 1))()
+        keep = [buf(x) for x in (pb, qb)]
+        check(self._l.hbh_dbg_pairing(self._h, n, keep[0][1], keep[1][1], ctypes.cast(out, ctypes.c_void_p)))
+        raw = bytes(out)[: n * 576]
+        return [raw[i * 576:(i + 1) * 576] for i in range(n)]
+
+
+# ------------------------------------------------------------------ wire-format helpers
+def g1_abi_from_uncompressed(b):
+    """pairing 0.14 G1Uncompressed (96 B, BE, 0x40 = infinity) -> ABI bytes."""
+    b = bytes(b)
+    if len(b) != 96:
+        raise ValueError("G1 uncompressed must be 96 bytes")
+    if b[0] & 0x40:
+        return bytes(96)
+    return b[0:48][::-1] + b[48:96][::-1]
+
+
+def g2_abi_from_uncompressed(b):
+    """pairing 0.14 G2Uncompressed (192 B: x.c1 x.c0 y.c1 y.c0, BE) -> ABI (x.c0 x.c1 y.c0 y.c1, LE)."""
+    b = bytes(b)
+    if len(b) != 192:
+        raise ValueError("G2 uncompressed must be 192 bytes")
+    if b[0] & 0x40:
+        return bytes(192)
+    return b[48:96][::-1] + b[0:48][::-1] + b[144:192][::-1] + b[96:144][::-1]
+
+
+def g1_uncompressed_from_abi(b):
+    b = bytes(b)
+    if not any(b):
+        return bytes([0x40]) + bytes(95)
+    return b[0:48][::-1] + b[48:96][::-1]
+
+
+def g2_uncompressed_from_abi(b):
+    b = bytes(b)
+    if not any(b):
+        return bytes([0x40]) + bytes(191)
+    return b[48:96][::-1] + b[0:48][::-1] + b[144:192][::-1] + b[96:144][::-1]

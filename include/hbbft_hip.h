@@ -1,0 +1,108 @@
+/* hbbft_hip.h -- C ABI of the MI355X batch engine for hbbft's BLS12-381 threshold-crypto hot path.
+ *
+ * This is the drop-in boundary.  hbbft itself never calls curve arithmetic: its
+ * three protocol modules call `threshold_crypto` 0.3 methods synchronously, one share at a time.
+ * Each entry point below is the batched replacement for one of those calls; a Rust binding
+ *  drains the shares a `Step` would verify into one call.
+ *
+ * Conventions
+ *  - Plain pointers + sizes, caller-owned buffers, nothing retained after return.
+ *  - Points are affine, canonical (non-Montgomery) little-endian integers:
+ *      G1 = x(48 B) || y(48 B)                         (HBH_G1_BYTES = 96)
+ *      G2 = x.c0 || x.c1 || y.c0 || y.c1 (48 B each)   (HBH_G2_BYTES = 192)
+ *    The point at infinity is all-zero bytes.  Points must be on the curve and in the prime-order
+ *    subgroup, as threshold_crypto's deserialisation guarantees for every point that reaches the
+ *    reference's verify calls; the engine does not re-check membership.
+ *  - Scalars (Fr) are 32-byte little-endian canonical integers.
+ *  - Verdicts are one byte per item (1 = valid, 0 = invalid), never an error: an invalid share is
+ *    a Fault in hbbft, not an Err (src/threshold_sign.rs:191-194, src/threshold_decrypt.rs:192-195).
+ *  - Every function returns an hbh_status; HBH_OK = 0.
+ *  - `_dev` variants take device pointers (HBM-resident inputs) and an optional hipStream_t
+ *    (passed as void*, NULL = the engine's stream); they are asynchronous on that stream.
+ *  - One engine handle binds one GPU.  Calls on one handle are serialised by the handle's mutex;
+ *    distinct handles may be used from distinct threads.
+ */
+#ifndef HBBFT_HIP_H
+#define HBBFT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBH_G1_BYTES 96
+#define HBH_G2_BYTES 192
+#define HBH_FR_BYTES 32
+
+typedef enum {
+  HBH_OK = 0,
+  HBH_ERR_ARG = 1,       /* null pointer / size out of range / index out of range */
+  HBH_ERR_DEVICE = 2,    /* HIP runtime error (message via hbh_last_error) */
+  HBH_ERR_NOMEM = 3,     /* device allocation failed */
+  HBH_ERR_NOT_ENOUGH_SHARES = 4,  /* threshold_crypto Error::NotEnoughShares */
+  HBH_ERR_DUPLICATE_ENTRY = 5     /* threshold_crypto Error::DuplicateEntry */
+} hbh_status;
+
+typedef struct hbh_engine hbh_engine;
+
+/* Engine lifetime.  `device` is a HIP device ordinal. */
+int hbh_engine_create(int device, hbh_engine** out);
+int hbh_engine_destroy(hbh_engine* eng);
+/* Last error message of this thread (static storage, never NULL). */
+const char* hbh_last_error(void);
+/* Number of HIP devices visible to this process. */
+int hbh_device_count(int* out);
+
+/* ---------------------------------------------------------------- pairing-equality checks
+ * Generic batched check  e(P1[i], Q1[q1_idx[i]]) == e(P2[i], Q2[q2_idx[i]])  for i < n,
+ * computed as one 2-pair multi-Miller loop + one final exponentiation per item.
+ * Q tables hold the G2 points shared by many items (H per document, W / H_uv per ciphertext);
+ * q*_idx == NULL means the identity map (table size must then be n).
+ * Replaces every pairing comparison on the path:
+ *   PublicKeyShare::verify_g2   (src/threshold_sign.rs:223)   P1=pk_i, Q1=H, P2=g1, Q2=sig_i
+ *   PublicKey::verify_g2        (src/threshold_sign.rs:264)   P1=pk,   Q1=H, P2=g1, Q2=sig
+ *   Ciphertext::verify          (src/threshold_decrypt.rs:142) P1=g1, Q1=W, P2=U, Q2=H_uv
+ *   verify_decryption_share     (src/threshold_decrypt.rs:227) P1=D_i, Q1=H_uv, P2=pk_i, Q2=W
+ */
+int hbh_verify_pairing_eq(hbh_engine* eng, size_t n,
+                          const uint8_t* p1, const uint8_t* q1_table, size_t nq1, const uint32_t* q1_idx,
+                          const uint8_t* p2, const uint8_t* q2_table, size_t nq2, const uint32_t* q2_idx,
+                          uint8_t* verdicts);
+
+/* PublicKeyShare::verify_g2(share, hash) batched (src/threshold_sign.rs:216-225):
+ *   verdict[i] = e(pk[i], hashes[doc_idx[i]]) == e(g1, sigs[i]). */
+int hbh_verify_sig_shares(hbh_engine* eng, size_t n, const uint8_t* pks, const uint8_t* sigs,
+                          const uint8_t* hashes, size_t ndocs, const uint32_t* doc_idx, uint8_t* verdicts);
+
+/* PublicKeyShare::verify_decryption_share(share, ct) batched (src/threshold_decrypt.rs:220-229):
+ *   verdict[i] = e(D[i], huv[ct_idx[i]]) == e(pk[i], w[ct_idx[i]]);
+ * huv = hash_g1_g2(U, V) is computed once per ciphertext on the host (the reference recomputes it
+ * per check, SURVEY §8a a8 -- the value is identical). */
+int hbh_verify_dec_shares(hbh_engine* eng, size_t n, const uint8_t* shares, const uint8_t* pks,
+                          const uint8_t* huv, const uint8_t* w, size_t ncts, const uint32_t* ct_idx,
+                          uint8_t* verdicts);
+
+/* Ciphertext::verify batched (src/threshold_decrypt.rs:142): verdict[i] = e(g1, w[i]) == e(u[i], huv[i]). */
+int hbh_verify_ciphertexts(hbh_engine* eng, size_t n, const uint8_t* u, const uint8_t* w,
+                           const uint8_t* huv, uint8_t* verdicts);
+
+/* Device-pointer variant of hbh_verify_pairing_eq (inputs already in HBM).  Asynchronous on
+ * `stream` (hipStream_t as void*, NULL = engine stream). */
+int hbh_verify_pairing_eq_dev(hbh_engine* eng, void* stream, size_t n,
+                              const void* d_p1, const void* d_q1_table, size_t nq1, const uint32_t* d_q1_idx,
+                              const void* d_p2, const void* d_q2_table, size_t nq2, const uint32_t* d_q2_idx,
+                              uint8_t* d_verdicts);
+
+/* ---------------------------------------------------------------- debug / test entry points
+ * hbh_dbg_pairing: out[i] = e(P[i], Q[i])^3 as 12 canonical Fp2 coefficients (c0.c0.c0, c0.c0.c1,
+ * c0.c1.c0, ... c1.c2.c1; 48 B LE each = 576 B) -- the pairing value itself, for parity tests
+ * against the oracle (the kernel's final exponentiation uses the exponent 3(p^12-1)/r). */
+int hbh_dbg_pairing(hbh_engine* eng, size_t n, const uint8_t* p, const uint8_t* q, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HBBFT_HIP_H */
