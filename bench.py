@@ -1,15 +1,26 @@
-"""Benchmark of the hot path: batched ThresholdSign share verification (PublicKeyShare::verify_g2,
-reference src/threshold_sign.rs:216-225) on MI355X, N=64 f=21, plus combine latency.
+"""Benchmark of the hot path on MI355X: batched ThresholdSign share verification
+(PublicKeyShare::verify_g2, reference src/threshold_sign.rs:216-225) at N=64 f=21, plus the
+combine latency of combine_and_verify_sig (src/threshold_sign.rs:249-270).
 
-One step = one batch of BATCH share checks resident in HBM -> verdict bytes in HBM, through the
-C ABI (hbh_verify_pairing_eq_dev).  Multi-GPU: one process per GPU, each rank verifies its own
-batch (shards by batch index, no collective on the data path; weak scaling).
+One step = one batch of 65,536 share checks (1,024 documents x 64 shares, BASELINE.json
+configs[1]) resident in HBM -> verdict bytes in HBM, through the C ABI
+(hbh_verify_pairing_eq_dev).  Multi-GPU: one process per GPU, every rank verifies its own batch
+(shards by batch index, no collective on the data path; weak scaling).
 
-Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §Measurement).
+Inputs are synthetic and seeded: a degree-21 master polynomial, public-key shares g1 * sk_i,
+1,024 document points H_m = g2 * r_m (uniform in G2 like hash_g2's output; hashing stays on the
+host in the reference flow and is not part of the path), shares sigma_{m,i} = sk_i * H_m, and one
+share per document replaced by a random G2 point (1/64 invalid).  Keys and shares are generated
+on the GPU with the engine's own scalar-multiplication kernels; verdicts are checked against the
+construction.
+
+Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import random
+import statistics
 import sys
 import time
 
@@ -21,60 +32,129 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 N_NODES, F_FAULTY = 64, 21
-BATCH = 65536  # BASELINE.json configs[1]
+T = F_FAULTY
+NDOCS = 1024
 METRIC = "verified BLS sig shares/sec (whole node) + combine latency, N=64 f=21"
-# Algorithmic work of one check: Fp-multiplications of the 2-pair
-# multi-Miller loop + final exponentiation, counted by tools/count_work.py; each Fp-mul of the
-# 14x28-bit representation = 2*14*14 v_mad_u64_u32 (product + Montgomery reduction).
-FP_MULS_PER_CHECK = None  # filled from hbbft_amd.workcount
-MADS_PER_FPMUL = 2 * 14 * 14
-PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12  # half-rate v_mad_u64_u32 on 256 CUs x 4 SIMD-32 @2.4 GHz
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+MADS_PER_FPMUL = 2 * 14 * 14          # 14 x 28-bit limbs: product + Montgomery reduction
+PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # v_mad_u64_u32 at half rate: 256 CU x 4 SIMD32 x 2.4 GHz
+G1_UNC = bytes.fromhex(
+    "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
+    "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
+G2_UNC = bytes.fromhex(
+    "13e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+    "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8"
+    "0606c4a02ea734cc32acd2b02bc28b99cb3e287e85a763af267492ab572e99ab3f370d275cec1da1aaa9075ff05f79be"
+    "0ce5d527727d6e118cc9cdc6da2e351aadfd9baa8cbdd3a76d429a695160d12c923ac9cc3baca289e193548608b82801")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_batch(n):
-    """Synthetic batch: the committed golden ThresholdSign instance (seeded keys, hash_g2 of
-    28-byte coin documents, valid / random-G2 / other-document / infinity shares) tiled to n
-    checks.  Inputs are data only; verdicts expected from the fixture."""
-    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
-    with open(os.path.join(ROOT, "tests", "golden", "threshold_sign_n10_t3.json")) as f:
-        d = json.load(f)
-    pks, sigs, didx, exp, hashes = [], [], [], [], []
-    for di, doc in enumerate(d["docs"]):
-        hashes.append(g2a(bytes.fromhex(doc["hash"])))
-        for s in doc["shares"]:
-            pks.append(g1a(bytes.fromhex(d["pk_shares"][s["idx"]])))
-            sigs.append(g2a(bytes.fromhex(s["sig"])))
-            didx.append(di)
-            exp.append(s["valid"])
-    m = len(pks)
-    sel = [i % m for i in range(n)]
-    pk = np.frombuffer(b"".join(pks[i] for i in sel), dtype=np.uint8)
-    sg = np.frombuffer(b"".join(sigs[i] for i in sel), dtype=np.uint8)
-    di = np.array([didx[i] for i in sel], dtype=np.int32)
-    ex = np.array([exp[i] for i in sel], dtype=np.uint8)
-    hs = np.frombuffer(b"".join(hashes), dtype=np.uint8)
-    return pk, sg, hs, di, ex
+def poly_eval(coeffs, x):
+    r = 0
+    for c in reversed(coeffs):
+        r = (r * x + c) % R_ORDER
+    return r
 
 
-def cpu_baseline(budget_s=15.0):
-    """Oracle (pure-Python restatement, 'port') timed on a bounded sample on one core."""
-    from oracle import bls12_381 as C
-    from oracle import tc
-    k = 0
-    pk = C.g1_mul(C.G1_GEN, 12345)
-    h = C.g2_mul(C.G2_GEN, 777)
-    sig = C.g2_mul(h, 12345)
+class Workload:
+    """Seeded ThresholdSign instance set, generated on the GPU (engine scalar multiplication)."""
+
+    def __init__(self, eng, batch, seed):
+        from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
+        rng = random.Random(seed)
+        self.g1, self.g2 = g1a(G1_UNC), g2a(G2_UNC)
+        self.coeffs = [rng.randrange(1, R_ORDER) for _ in range(T + 1)]
+        self.sk = [poly_eval(self.coeffs, i + 1) for i in range(N_NODES)]
+        self.pks = eng.g1_mul([self.g1] * N_NODES, self.sk)
+        self.master_pk = eng.g1_mul([self.g1], [self.coeffs[0]])[0]
+        ndocs = max(1, batch // N_NODES)
+        self.hashes = eng.g2_mul([self.g2] * ndocs, [rng.randrange(1, R_ORDER) for _ in range(ndocs)])
+        doc_idx = np.arange(batch, dtype=np.int64) // N_NODES
+        node = np.arange(batch, dtype=np.int64) % N_NODES
+        bad = {m * N_NODES + (m * 37) % N_NODES for m in range(ndocs)}
+        bases, scal = [], []
+        for i in range(batch):
+            if i in bad:
+                bases.append(self.g2)
+                scal.append(rng.randrange(1, R_ORDER))
+            else:
+                bases.append(self.hashes[doc_idx[i]])
+                scal.append(self.sk[node[i]])
+        t0 = time.time()
+        self.sigs = eng.g2_mul(bases, scal)
+        log("generated %d shares on the GPU in %.2f s" % (batch, time.time() - t0))
+        self.expected = np.array([0 if i in bad else 1 for i in range(batch)], dtype=np.uint8)
+        self.doc_idx = doc_idx.astype(np.int32)
+        self.node = node
+        self.pk_batch = b"".join(self.pks[j] for j in node)
+        self.sig_batch = b"".join(self.sigs)
+        self.hash_table = b"".join(self.hashes)
+
+
+def cpu_baseline(w, budget_s=12.0):
+    """Reference-equivalent CPU path (oracle/c/bls_cpu.c: pairing 0.14 algorithms, two pairings per
+    check) on a bounded sample of the same workload, one thread and all host threads."""
+    from oracle import cbls
+    if not os.path.exists(cbls.LIB_PATH):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    n1 = 200
+    pk, sg = w.pk_batch[:96 * n1], w.sig_batch[:192 * n1]
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or k == 0:
-        assert tc.verify_g2(pk, sig, h)
-        k += 1
-    dt = time.perf_counter() - t0
-    return {"value": k / dt, "unit": "shares/s", "cores": 1, "kind": "port",
-            "sample": "%d verify_g2 checks (pure-Python oracle, 1 thread)" % k}
+    v = cbls.verify_g2_batch(pk, sg, w.hash_table, w.doc_idx[:n1], threads=1)
+    st = time.perf_counter() - t0
+    assert (v == w.expected[:n1]).all(), "CPU baseline verdicts disagree"
+    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(16, ncpu))
+    n2 = int(min(len(w.expected), max(threads * 8, (budget_s / (st / n1)) * threads * 0.5)))
+    t0 = time.perf_counter()
+    v = cbls.verify_g2_batch(w.pk_batch[:96 * n2], w.sig_batch[:192 * n2], w.hash_table, w.doc_idx[:n2],
+                             threads=threads)
+    mt = time.perf_counter() - t0
+    assert (v == w.expected[:n2]).all(), "CPU baseline verdicts disagree"
+    # combine latency on the CPU: interpolate 22 G2 shares + master verify_g2
+    idx = [k for k in range(N_NODES) if w.expected[k]][: T + 1]
+    pts = [w.sigs[k] for k in idx]
+    t0 = time.perf_counter()
+    rc, sig = cbls.combine_g2(T, idx, pts)
+    ok = cbls.verify_g2(w.master_pk, sig, w.hashes[0])
+    comb_ms = (time.perf_counter() - t0) * 1e3
+    assert rc == 0 and ok
+    return {"value": n2 / mt, "unit": "shares/s", "cores": threads, "kind": "port",
+            "sample": "%d verify_g2 checks of the same batch on %d threads (and %d on 1 thread: %.1f shares/s); "
+                      "C restatement of pairing 0.14 (two pairings per check)" % (n2, threads, n1, n1 / st),
+            "single_thread_value": n1 / st, "combine_latency_ms": comb_ms}
+
+
+def combine_latency(eng, w, reps=7):
+    """combine_and_verify_sig for one document: interpolate the first t+1 valid shares (G2 MSM
+    with Lagrange coefficients) + verify the result against the master key; host-to-host wall
+    time through the C ABI (median of reps).  Also the batched rate (one combine per document)."""
+    idx = [k for k in range(N_NODES) if w.expected[k]][: T + 1]
+    pts = [w.sigs[k] for k in idx]
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out, st = eng.interpolate_g2(T, [idx], [pts])
+        v = eng.verify_sig_shares([w.master_pk], [out[0]], [w.hashes[0]], [0])
+        times.append((time.perf_counter() - t0) * 1e3)
+        assert st == [0] and v == b"\x01", "combined signature does not verify"
+    ndocs = len(w.hashes)
+    allidx, allpts = [], []
+    for m in range(ndocs):
+        ids = [k for k in range(N_NODES) if w.expected[m * N_NODES + k]][: T + 1]
+        allidx.append(ids)
+        allpts.append([w.sigs[m * N_NODES + k] for k in ids])
+    t0 = time.perf_counter()
+    out, st = eng.interpolate_g2(T, allidx, allpts)
+    bt = time.perf_counter() - t0
+    assert all(s == 0 for s in st)
+    v = eng.verify_sig_shares([w.master_pk] * ndocs, out, w.hashes, list(range(ndocs)))
+    assert all(v), "a batched combined signature does not verify"
+    return statistics.median(times), ndocs / bt
 
 
 def main():
@@ -82,8 +162,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--batch", type=int, default=NDOCS * N_NODES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-combine", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,81 +175,87 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    from hbbft_amd import workcount
+    from hbbft_amd._lib import STAGE_PAIRING, STAGE_PREPARE
     from hbbft_amd.engine import Engine
     eng = Engine(local)
     n = args.batch
-    pk, sg, hs, di, ex = make_batch(n)
-    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
-    g1_unc = bytes.fromhex(  # G1 generator (pairing 0.14 uncompressed encoding)
-        "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
-        "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
-    g1 = np.frombuffer(g1a(g1_unc) * n, dtype=np.uint8)
-    d_pk = torch.from_numpy(pk.copy()).to(dev)
-    d_sg = torch.from_numpy(sg.copy()).to(dev)
-    d_hs = torch.from_numpy(hs.copy()).to(dev)
-    d_di = torch.from_numpy(di.copy()).to(dev)
-    d_g1 = torch.from_numpy(g1.copy()).to(dev)
+    w = Workload(eng, n, seed=20261016 + rank)
+
+    def to_dev(b):
+        return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).to(dev)
+
+    d_pk = to_dev(w.pk_batch)
+    d_sg = to_dev(w.sig_batch)
+    d_hs = to_dev(w.hash_table)
+    d_di = torch.from_numpy(w.doc_idx.copy()).to(dev)
+    d_g1 = to_dev(w.g1 * n)
     d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
-    nh = hs.size // 192
-    # a dedicated stream: the engine launches on it, and the timing events are recorded on it
-    ts = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(ts)
+    nh = len(w.hashes)
+    ts = torch.cuda.Stream(dev)  # the engine launches on this stream; timing events are recorded on it
+    torch.cuda.synchronize(dev)
     stream = ts.cuda_stream
-    assert stream, "need a non-null stream handle"
 
     def step():
         eng.verify_pairing_eq_dev(stream, n, d_pk.data_ptr(), d_hs.data_ptr(), nh, d_di.data_ptr(),
                                   d_g1.data_ptr(), d_sg.data_ptr(), n, None, d_v.data_ptr())
 
-    t0 = time.time()
     step()
     torch.cuda.synchronize(dev)
-    log("first step %.3f s" % (time.time() - t0))
-    ok = bool((d_v.cpu().numpy() == ex).all())
+    ok = bool((d_v.cpu().numpy() == w.expected).all())
     if not ok:
-        raise SystemExit("verdict mismatch against the expected pattern")
+        raise SystemExit("verdict mismatch against the construction")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    eng.set_profiling(True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    w0 = time.perf_counter()
-    ev0.record()
+    ev0.record(ts)
     for _ in range(args.steps):
         step()
-    ev1.record()
+    ev1.record(ts)
     torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - w0
     if world > 1:
         dist.barrier()
     ms = ev0.elapsed_time(ev1)
+    pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
+    prep_ms, prep_n = eng.stage_time(STAGE_PREPARE)
+    eng.set_profiling(False)
     t = torch.tensor([ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms_step = float(t.item()) / args.steps
     value = n * world / (ms_step / 1e3)
-    ok = ok and bool((d_v.cpu().numpy() == ex).all())
+    ok = ok and bool((d_v.cpu().numpy() == w.expected).all())
+
     if rank == 0:
-        from hbbft_amd import workcount
-        fpm = workcount.FP_MULS_PER_CHECK
-        achieved = n * fpm * MADS_PER_FPMUL / (ms_step / 1e3) / 1e12
+        kern_ms = pair_ms / max(pair_n, 1)
+        fpm = workcount.MILLER_2PAIR + workcount.FINAL_EXP
+        achieved = n * fpm * MADS_PER_FPMUL / (kern_ms / 1e3) / 1e12
         out = {
             "metric": METRIC, "value": value, "unit": "shares/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 14x28-bit limbs)",
-            "data": "synthetic (seeded golden ThresholdSign instance tiled; 20% invalid shares)",
-            "config": {"workload": "ThresholdSign share verification batch", "batch_per_gpu": n,
-                       "n_nodes": N_NODES, "f": F_FAULTY, "parallelism": "shard-by-batch x%d" % world},
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
+            "data": "synthetic, seeded (degree-21 key, 1024 document points, 1/64 invalid shares; generated on GPU)",
+            "config": {"workload": "ThresholdSign share verification, BASELINE configs[1]", "batch_per_gpu": n,
+                       "documents_per_gpu": nh, "n_nodes": N_NODES, "f": F_FAULTY,
+                       "parallelism": "shard-by-batch x%d" % world},
             "verdicts_ok": ok,
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_TMAD, "unit": "T int32-MAD/s",
-                         "frac": achieved / PEAK_TMAD, "traffic": None,
-                         "note": "whole step (line precompute + pairing kernel); per-check Fp-mul %d" % fpm},
-            "wall_s_timed": wall,
+            "roofline": {"bound": "valu", "kernel": "hb::k_pairing_eq", "achieved": achieved, "peak": PEAK_TMAD,
+                         "unit": "T int32-MAD/s", "frac": achieved / PEAK_TMAD, "traffic": None,
+                         "kernel_ms": kern_ms, "prepare_ms": prep_ms / max(prep_n, 1),
+                         "work_per_check_fpmul": fpm,
+                         "note": "achieved = checks x (multi-Miller + final-exp Fp-mul) x 392 MAD / kernel time"},
         }
+        if not args.no_combine:
+            lat, rate = combine_latency(eng, w)
+            out["combine_latency_ms"] = lat
+            out["combines_per_s_batched"] = rate
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline()
+            out["cpu_baseline"] = cpu_baseline(w)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

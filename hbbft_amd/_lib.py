@@ -29,7 +29,16 @@ SIGNATURES = [
     ("hbh_verify_ciphertexts", _I, [_P, _SZ, _P, _P, _P, _P]),
     ("hbh_verify_pairing_eq_dev", _I, [_P, _P, _SZ, _P, _P, _SZ, _P, _P, _P, _SZ, _P, _P]),
     ("hbh_dbg_pairing", _I, [_P, _SZ, _P, _P, _P]),
+    ("hbh_interpolate_g2", _I, [_P, _SZ, _I, _P, _P, _P, _P]),
+    ("hbh_interpolate_g1", _I, [_P, _SZ, _I, _P, _P, _P, _P]),
+    ("hbh_g1_mul", _I, [_P, _SZ, _P, _P, _P]),
+    ("hbh_g2_mul", _I, [_P, _SZ, _P, _P, _P]),
+    ("hbh_bivar_row", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),
+    ("hbh_bivar_ack_check", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P, _P, _P]),
+    ("hbh_engine_set_profiling", _I, [_P, _I]),
+    ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),
 ]
+STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
 
 _lib = None
 

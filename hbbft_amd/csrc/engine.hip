@@ -1,5 +1,5 @@
 // Host side of the C ABI (include/hbbft_hip.h): device/stream/workspace management and batch
-// orchestration of the HIP kernels in kernels.hpp.  No CPU fallback: every verdict comes from
+// orchestration of the HIP kernels behind launch.hpp.  No CPU fallback: every verdict comes from
 // the GPU; without a usable device the calls fail with HBH_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 
@@ -10,9 +10,7 @@
 #include <vector>
 
 #include "../../include/hbbft_hip.h"
-#include "kernels.hpp"
-
-using namespace hb;
+#include "launch.hpp"
 
 namespace {
 
@@ -51,33 +49,67 @@ struct DevBuf {
   }
 };
 
-inline int pad64(size_t n) { return (int)((n + 63) / 64 * 64); }
-
 }  // namespace
+
+// Per-stage kernel timing (hbh_engine_set_profiling): HIP events recorded around each stage's
+// launch on the stream it runs on, summed by hbh_engine_stage_time.
+struct StageTimer {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[HBH_NUM_STAGES];
+  hipEvent_t begin(hipStream_t s, int stage, bool on) {
+    if (!on) return nullptr;
+    hipEvent_t a, b;
+    if (hipEventCreate(&a) != hipSuccess) return nullptr;
+    if (hipEventCreate(&b) != hipSuccess) { (void)hipEventDestroy(a); return nullptr; }
+    (void)hipEventRecord(a, s);
+    ev[stage].push_back({a, b});
+    return b;
+  }
+  void end(hipStream_t s, hipEvent_t b) {
+    if (b) (void)hipEventRecord(b, s);
+  }
+  void clear() {
+    for (auto& v : ev) {
+      for (auto& p : v) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+      }
+      v.clear();
+    }
+  }
+};
 
 struct hbh_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  bool profiling = false;
+  StageTimer timer;
   // workspaces
-  DevBuf coef1, coef2, inf1, inf2;
+  DevBuf coef1, coef2, inf1, inf2, work, status;
   // staging for host-pointer entry points
-  DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v;
+  DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
 };
 
 namespace {
 
-size_t coef_bytes(size_t npts) { return (size_t)MILLER_STEPS * LINE_Q4 * pad64(npts) * sizeof(uint4); }
+using hbl::line_table_bytes;
 
-int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts, size_t n, DevBuf& coef, DevBuf& inf) {
-  if (n == 0) return HBH_OK;
-  HBH_CHECK(coef.ensure(coef_bytes(n)));
-  HBH_CHECK(inf.ensure(n));
-  const int threads = 256;
-  const int blocks = (int)((n + threads - 1) / threads);
-  hipLaunchKernelGGL(k_g2_prepare, dim3(blocks), dim3(threads), 0, s, (int)n, (const uint32_t*)d_pts, pad64(n),
-                     (uint4*)coef.p, (uint8_t*)inf.p);
-  HBH_CHECK(hipGetLastError());
+// Line tables for up to two G2 point sets, in one launch.
+int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, DevBuf& coef0, DevBuf& inf0,
+                   const void* d_pts1 = nullptr, size_t n1 = 0, DevBuf* coef1 = nullptr, DevBuf* inf1 = nullptr) {
+  if (n0 + n1 == 0) return HBH_OK;
+  if (n0) {
+    HBH_CHECK(coef0.ensure(line_table_bytes(n0)));
+    HBH_CHECK(inf0.ensure(n0));
+  }
+  if (n1) {
+    HBH_CHECK(coef1->ensure(line_table_bytes(n1)));
+    HBH_CHECK(inf1->ensure(n1));
+  }
+  hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
+  HBH_CHECK(hbl::g2_prepare(s, (int)n0, d_pts0, coef0.p, (uint8_t*)inf0.p, (int)n1, d_pts1, n1 ? coef1->p : nullptr,
+                            n1 ? (uint8_t*)inf1->p : nullptr));
+  e->timer.end(s, t);
   return HBH_OK;
 }
 
@@ -86,16 +118,12 @@ int run_pairing_eq_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1,
                        uint8_t* d_v) {
   if (n == 0) return HBH_OK;
   if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
-  int rc = launch_prepare(e, s, d_q1, nq1, e->coef1, e->inf1);
+  int rc = launch_prepare(e, s, d_q1, nq1, e->coef1, e->inf1, d_q2, nq2, &e->coef2, &e->inf2);
   if (rc) return rc;
-  rc = launch_prepare(e, s, d_q2, nq2, e->coef2, e->inf2);
-  if (rc) return rc;
-  const int threads = 256;
-  const int blocks = (int)((n + threads - 1) / threads);
-  hipLaunchKernelGGL(k_pairing_eq, dim3(blocks), dim3(threads), 0, s, (int)n, (const uint32_t*)d_p1,
-                     (const uint4*)e->coef1.p, pad64(nq1), (const uint8_t*)e->inf1.p, d_i1, (const uint32_t*)d_p2,
-                     (const uint4*)e->coef2.p, pad64(nq2), (const uint8_t*)e->inf2.p, d_i2, d_v);
-  HBH_CHECK(hipGetLastError());
+  hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
+  HBH_CHECK(hbl::pairing_eq(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2, e->coef2.p,
+                            (int)nq2, (const uint8_t*)e->inf2.p, d_i2, d_v));
+  e->timer.end(s, t);
   return HBH_OK;
 }
 
@@ -145,17 +173,13 @@ int run_pairing_eq_host(hbh_engine* e, size_t n, const uint8_t* p1, const uint8_
   return HBH_OK;
 }
 
-// G1 generator in the ABI format (canonical LE words), built once on the host.
+// G1 generator in the ABI format (canonical little-endian x || y).
 const std::vector<uint8_t>& g1_generator_bytes() {
-  static std::vector<uint8_t> g = [] {
-    std::vector<uint8_t> b(HBH_G1_BYTES);
-    Fp x = fp_from_mont(fp_const(G1X_M)), y = fp_from_mont(fp_const(G1Y_M));
-    uint32_t w[24];
-    fp_limbs_to_words(x, w);
-    fp_limbs_to_words(y, w + 12);
-    std::memcpy(b.data(), w, sizeof(w));
-    return b;
-  }();
+  static const uint32_t w[24] = {
+      0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu,
+      0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u, 0x46c5e7e1u, 0x0caa2329u, 0xa2888ae4u, 0xd03cc744u,
+      0x2c04b3edu, 0x00db18cbu, 0xd5d00af6u, 0xfcf5e095u, 0x741d8ae4u, 0xa09e30edu, 0xe3aaa0f1u, 0x08b3f481u};
+  static std::vector<uint8_t> g((const uint8_t*)w, (const uint8_t*)w + sizeof(w));
   return g;
 }
 
@@ -205,8 +229,9 @@ int hbh_engine_destroy(hbh_engine* e) {
   if (!e) return HBH_OK;
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
-  for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2,
-                    &e->in_i2, &e->out_v})
+  e->timer.clear();
+  for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->in_p1, &e->in_q1, &e->in_i1,
+                    &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v, &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x})
     b->release();
   (void)hipStreamDestroy(e->stream);
   delete e;
@@ -276,12 +301,207 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
   HBH_CHECK(hipMemcpyAsync(e->in_q1.p, q, n * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
   int rc = launch_prepare(e, s, e->in_q1.p, n, e->coef1, e->inf1);
   if (rc) return rc;
-  const int threads = 256;
-  hipLaunchKernelGGL(k_dbg_pairing, dim3((unsigned)((n + threads - 1) / threads)), dim3(threads), 0, s, (int)n,
-                     (const uint32_t*)e->in_p1.p, (const uint4*)e->coef1.p, pad64(n), (const uint8_t*)e->inf1.p,
-                     (uint32_t*)e->out_v.p);
-  HBH_CHECK(hipGetLastError());
+  HBH_CHECK(hbl::pairing_value(s, (int)n, e->in_p1.p, e->coef1.p, (const uint8_t*)e->inf1.p, (uint32_t*)e->out_v.p));
   HBH_CHECK(hipMemcpyAsync(out, e->out_v.p, n * 576, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int hbh_engine_set_profiling(hbh_engine* e, int on) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  HBH_CHECK(hipStreamSynchronize(e->stream));
+  e->timer.clear();
+  e->profiling = on != 0;
+  return HBH_OK;
+}
+
+int hbh_engine_stage_time(hbh_engine* e, int stage, double* total_ms, int* launches) {
+  if (!e || !total_ms || !launches || stage < 0 || stage >= HBH_NUM_STAGES) return fail(HBH_ERR_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  double sum = 0;
+  for (auto& p : e->timer.ev[stage]) {
+    HBH_CHECK(hipEventSynchronize(p.second));
+    float ms = 0;
+    HBH_CHECK(hipEventElapsedTime(&ms, p.first, p.second));
+    sum += ms;
+  }
+  *total_ms = sum;
+  *launches = (int)e->timer.ev[stage].size();
+  return HBH_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- curve entry points
+namespace {
+int check_t(int t) { return (t < 0 || t > 4096) ? fail(HBH_ERR_ARG, "threshold out of range") : HBH_OK; }
+
+template <class Launch>
+int run_mul(hbh_engine* e, size_t n, const uint8_t* pts, size_t pt_bytes, const uint8_t* scalars, uint8_t* out,
+            Launch launch) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (n == 0) return HBH_OK;
+  if (!pts || !scalars || !out) return fail(HBH_ERR_ARG, "null pointer");
+  if (n > (size_t)1 << 28) return fail(HBH_ERR_ARG, "batch too large");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  HBH_CHECK(e->in_a.ensure(n * pt_bytes));
+  HBH_CHECK(e->in_b.ensure(n * HBH_FR_BYTES));
+  HBH_CHECK(e->out_x.ensure(n * pt_bytes));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, pts, n * pt_bytes, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, scalars, n * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
+  hipEvent_t t = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(launch(s, (int)n, e->in_a.p, (const uint32_t*)e->in_b.p, e->out_x.p));
+  e->timer.end(s, t);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * pt_bytes, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out, int* status,
+               bool g2) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (ncomb == 0) return HBH_OK;
+  if (!idx || !pts || !out || !status) return fail(HBH_ERR_ARG, "null pointer");
+  const size_t m = (size_t)t + 1, pb = g2 ? HBH_G2_BYTES : HBH_G1_BYTES;
+  if (ncomb * m > (size_t)1 << 26) return fail(HBH_ERR_ARG, "batch too large");
+  // x_k = idx_k + 1 as a small Fr integer (threshold_crypto into_fr_plus_1)
+  std::vector<uint32_t> xs(ncomb * m);
+  for (size_t k = 0; k < ncomb * m; k++) {
+    if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
+    xs[k] = idx[k] + 1;
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
+  HBH_CHECK(e->in_b.ensure(ncomb * m * pb));
+  HBH_CHECK(e->out_x.ensure(ncomb * pb));
+  HBH_CHECK(e->status.ensure(ncomb * sizeof(int)));
+  HBH_CHECK(e->work.ensure(hbl::combine_work_bytes((int)ncomb, (int)m, g2)));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xs.data(), ncomb * m * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, pts, ncomb * m * pb, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  if (g2)
+    HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->work.p, e->out_x.p,
+                              (int*)e->status.p));
+  else
+    HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->work.p, e->out_x.p,
+                              (int*)e->status.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * pb, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int hbh_g1_mul(hbh_engine* e, size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out) {
+  return run_mul(e, n, pts, HBH_G1_BYTES, scalars, out, hbl::g1_mul);
+}
+int hbh_g2_mul(hbh_engine* e, size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out) {
+  return run_mul(e, n, pts, HBH_G2_BYTES, scalars, out, hbl::g2_mul);
+}
+int hbh_interpolate_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out,
+                       int* status) {
+  return run_interp(e, ncomb, t, idx, pts, out, status, true);
+}
+int hbh_interpolate_g1(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out,
+                       int* status) {
+  return run_interp(e, ncomb, t, idx, pts, out, status, false);
+}
+
+int hbh_bivar_row(hbh_engine* e, size_t nrow, int t, size_t nparts, const uint8_t* commits, const uint32_t* part_idx,
+                  const uint32_t* xs, uint8_t* out) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (nrow == 0) return HBH_OK;
+  if (!commits || !part_idx || !xs || !out) return fail(HBH_ERR_ARG, "null pointer");
+  const size_t ncoef = (size_t)(t + 1) * (t + 2) / 2;
+  for (size_t r = 0; r < nrow; r++)
+    if (part_idx[r] >= nparts) return fail(HBH_ERR_ARG, "part index out of range");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const size_t nout = nrow * (t + 1);
+  HBH_CHECK(e->in_a.ensure(nparts * ncoef * HBH_G1_BYTES));
+  HBH_CHECK(e->in_b.ensure(nrow * 4));
+  HBH_CHECK(e->in_c.ensure(nrow * 4));
+  HBH_CHECK(e->out_x.ensure(nout * HBH_G1_BYTES));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, commits, nparts * ncoef * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, part_idx, nrow * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_c.p, xs, nrow * 4, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, e->in_a.p, (const uint32_t*)e->in_b.p, (const uint32_t*)e->in_c.p,
+                           e->out_x.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, nout * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const uint8_t* commits,
+                        const uint32_t* part_idx, const uint32_t* xs, const uint32_t* ys, const uint8_t* vals,
+                        uint8_t* verdicts) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (nack == 0) return HBH_OK;
+  if (!commits || !part_idx || !xs || !ys || !vals || !verdicts) return fail(HBH_ERR_ARG, "null pointer");
+  const size_t ncoef = (size_t)(t + 1) * (t + 2) / 2;
+  // one row(x) per distinct (part, x): evaluate(x, y) = sum_j row(x)_j y^j
+  std::vector<uint32_t> row_part, row_x, row_of(nack);
+  {
+    std::vector<std::pair<uint64_t, uint32_t>> seen;
+    for (size_t a = 0; a < nack; a++) {
+      if (part_idx[a] >= nparts) return fail(HBH_ERR_ARG, "part index out of range");
+      const uint64_t key = ((uint64_t)part_idx[a] << 32) | xs[a];
+      uint32_t r = 0xffffffffu;
+      for (auto& kv : seen)
+        if (kv.first == key) { r = kv.second; break; }
+      if (r == 0xffffffffu) {
+        r = (uint32_t)row_part.size();
+        seen.push_back({key, r});
+        row_part.push_back(part_idx[a]);
+        row_x.push_back(xs[a]);
+      }
+      row_of[a] = r;
+    }
+  }
+  const size_t nrow = row_part.size();
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  HBH_CHECK(e->in_a.ensure(nparts * ncoef * HBH_G1_BYTES));
+  HBH_CHECK(e->in_b.ensure(nrow * 8 + nack * 8));
+  HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
+  HBH_CHECK(e->work.ensure(nrow * (t + 1) * HBH_G1_BYTES));
+  HBH_CHECK(e->out_v.ensure(nack));
+  uint32_t* d_rp = (uint32_t*)e->in_b.p;
+  uint32_t* d_rx = d_rp + nrow;
+  uint32_t* d_ro = d_rx + nrow;
+  uint32_t* d_y = d_ro + nack;
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, commits, nparts * ncoef * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_rp, row_part.data(), nrow * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_rx, row_x.data(), nrow * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_ro, row_of.data(), nack * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_y, ys, nack * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, e->in_a.p, d_rp, d_rx, e->work.p));
+  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, (uint8_t*)e->out_v.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, nack, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }

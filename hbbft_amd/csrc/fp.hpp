@@ -25,7 +25,7 @@
 // instruction cache, and the Fp12-level code above is a compact call sequence.  Fully inlined, one
 // final exponentiation is >2 MB of code and takes hipcc tens of minutes.
 #if defined(__HIPCC__) || defined(__HIP__)
-#define HB_MULFN __host__ __device__ __noinline__
+#define HB_MULFN static __host__ __device__ __noinline__
 #else
 #define HB_MULFN static
 #endif

@@ -46,11 +46,25 @@ __device__ __forceinline__ Line load_line(const uint4* __restrict__ coef, int st
   return l;
 }
 
-// Walk T over the Miller loop of Q and store its 68 lines.
-__global__ void __launch_bounds__(256) k_g2_prepare(int n, const uint32_t* __restrict__ pts, int stride,
-                                                    uint4* __restrict__ coef, uint8_t* __restrict__ inf) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// Walk T over the Miller loop of Q and store its 68 lines.  Two independent point sets share one
+// launch (the per-document H table and the per-share G2 points): the small set's latency-bound
+// walk then overlaps the large one instead of adding a serial launch.
+struct PrepSet {
+  int n;
+  const uint32_t* pts;
+  int stride;
+  uint4* coef;
+  uint8_t* inf;
+};
+__global__ void __launch_bounds__(256) k_g2_prepare(PrepSet s0, PrepSet s1) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool first = i < s0.n;
+  if (!first) i -= s0.n;
+  if (!first && i >= s1.n) return;
+  const uint32_t* pts = first ? s0.pts : s1.pts;
+  const int stride = first ? s0.stride : s1.stride;
+  uint4* coef = first ? s0.coef : s1.coef;
+  uint8_t* inf = first ? s0.inf : s1.inf;
   G2Aff q = g2_from_words(pts + (size_t)i * G2_WORDS);
   inf[i] = q.inf ? 1 : 0;
   if (q.inf) { q.x = f2_one(); q.y = f2_one(); }  // dummy walk; the pair is masked out

@@ -1,0 +1,50 @@
+// Host-side launchers of the HIP kernels.  Each kernel family lives in its own translation unit
+// (k_pairing.hip, k_curve.hip) so the Makefile compiles them in parallel; engine.hip owns the
+// C ABI, device buffers and streams and calls only these functions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace hbl {
+
+constexpr int HBL_DUPLICATE = 5;  // == HBH_ERR_DUPLICATE_ENTRY
+constexpr int MILLER_STEPS = 68;
+constexpr int LINE_Q4 = 21;  // 16-byte chunks per line (3 Fp2 x 14 limbs)
+inline int pad64(size_t n) { return (int)((n + 63) / 64 * 64); }
+inline size_t line_table_bytes(size_t npts) { return (size_t)MILLER_STEPS * LINE_Q4 * pad64(npts) * 16; }
+
+// --------------------------------------------------------------- pairing (k_pairing.hip)
+// Miller-loop line tables of up to two G2 point sets (ABI G2 words) in one launch.
+hipError_t g2_prepare(hipStream_t s, int n0, const void* pts0, void* coef0, uint8_t* inf0, int n1, const void* pts1,
+                      void* coef1, uint8_t* inf1);
+// verdict[i] = e(P1_i, Q1[idx1_i]) == e(P2_i, Q2[idx2_i]) from prepared line tables.
+hipError_t pairing_eq(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
+                      const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,
+                      const uint32_t* idx2, uint8_t* verdict);
+// out[i] = e(P_i, Q_i)^3 as 144 canonical words (debug / parity).
+hipError_t pairing_value(hipStream_t s, int n, const void* p, const void* coef, const uint8_t* inf, uint32_t* out);
+
+// --------------------------------------------------------------- curve / MSM (k_curve.hip)
+// out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).
+hipError_t g1_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars, void* out);
+hipError_t g2_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars, void* out);
+// Lagrange interpolation at 0 (threshold_crypto interpolate) of `ncomb` combines of m = t+1
+// samples each: x[c*m + k] = idx + 1 (Fr, small integers), pts[c*m + k] the samples.
+// status[c] (zeroed by the caller) becomes HBL_DUPLICATE when two x coincide.  work: scratch of
+// combine_work_bytes().  out: ncomb affine points (ABI words).
+hipError_t combine_g1(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* work, void* out,
+                      int* status);
+hipError_t combine_g2(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* work, void* out,
+                      int* status);
+size_t combine_work_bytes(int ncomb, int m, int g2);
+// BivarCommitment::row(x) (t+1 outputs) for nrow (part, x) pairs; commit = (t+1)(t+2)/2 G1 points
+// per part.  out[r*(t+1) + i].
+hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const uint32_t* part_idx, const uint32_t* xs,
+                     void* out);
+// BivarCommitment::evaluate(x, y) == g1 * val for nack checks, given the rows R = row(x) of each
+// check's part: verdict[a] = (sum_j R[row_idx[a]][j] * y^j == g1 * val[a]).
+hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
+                       const uint32_t* vals, uint8_t* verdict);
+
+}  // namespace hbl

@@ -115,6 +115,88 @@ class Engine:
                                                 vp(d_i1) if d_i1 else None, vp(d_p2), vp(d_q2), nq2,
                                                 vp(d_i2) if d_i2 else None, vp(d_v)))
 
+    # ------------------------------------------------------------ combine / scalar mult / DKG
+    def _interp(self, fn, size, t, idx, pts):
+        """idx: [[node index] * (t+1)] per combine; pts: matching point bytes (flat or nested)."""
+        ncomb = len(idx)
+        flat_idx = [int(i) for row in idx for i in row]
+        if any(len(row) != t + 1 for row in idx):
+            raise ValueError("each combine needs exactly t+1 samples")
+        pb = _join([p for row in pts for p in row] if ncomb and isinstance(pts[0], (list, tuple)) else pts, size)
+        if len(pb) != ncomb * (t + 1) * size:
+            raise ValueError("point count mismatch")
+        ia, pia = _u32(flat_idx, len(flat_idx))
+        out = (ctypes.c_uint8 * max(ncomb * size, 1))()
+        st = (ctypes.c_int * max(ncomb, 1))()
+        keep = buf(pb)
+        check(fn(self._h, ncomb, t, pia, keep[1], ctypes.cast(out, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [raw[c * size:(c + 1) * size] for c in range(ncomb)], list(st)[:ncomb]
+
+    def interpolate_g2(self, t, idx, pts):
+        """PublicKeySet::combine_signatures batch (src/threshold_sign.rs:249-259): (points, status)."""
+        return self._interp(self._l.hbh_interpolate_g2, G2_BYTES, t, idx, pts)
+
+    def interpolate_g1(self, t, idx, pts):
+        """G1 interpolation of PublicKeySet::decrypt (src/threshold_decrypt.rs:242-250)."""
+        return self._interp(self._l.hbh_interpolate_g1, G1_BYTES, t, idx, pts)
+
+    def _mul(self, fn, size, pts, scalars):
+        pb = _join(pts, size)
+        n = len(pb) // size
+        sb = b"".join(int(k).to_bytes(32, "little") for k in scalars)
+        if len(sb) != 32 * n:
+            raise ValueError("scalar count mismatch")
+        out = (ctypes.c_uint8 * max(n * size, 1))()
+        keep = [buf(pb), buf(sb)]
+        check(fn(self._h, n, keep[0][1], keep[1][1], ctypes.cast(out, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [raw[i * size:(i + 1) * size] for i in range(n)]
+
+    def g1_mul(self, pts, scalars):
+        return self._mul(self._l.hbh_g1_mul, G1_BYTES, pts, scalars)
+
+    def g2_mul(self, pts, scalars):
+        return self._mul(self._l.hbh_g2_mul, G2_BYTES, pts, scalars)
+
+    def bivar_row(self, t, commits, part_idx, xs):
+        """BivarCommitment::row(x) (src/sync_key_gen.rs:496) for each (part, x)."""
+        cb = _join([c for part in commits for c in part], G1_BYTES)
+        nrow = len(part_idx)
+        pa, ppa = _u32(part_idx, nrow)
+        xa, pxa = _u32(xs, nrow)
+        out = (ctypes.c_uint8 * max(nrow * (t + 1) * G1_BYTES, 1))()
+        keep = buf(cb)
+        check(self._l.hbh_bivar_row(self._h, nrow, t, len(commits), keep[1], ppa, pxa, ctypes.cast(out, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [[raw[(r * (t + 1) + i) * G1_BYTES:(r * (t + 1) + i + 1) * G1_BYTES] for i in range(t + 1)]
+                for r in range(nrow)]
+
+    def bivar_ack_check(self, t, commits, part_idx, xs, ys, vals):
+        """BivarCommitment::evaluate(x, y) == g1 * val (src/sync_key_gen.rs:542) per ack."""
+        cb = _join([c for part in commits for c in part], G1_BYTES)
+        n = len(part_idx)
+        pa, ppa = _u32(part_idx, n)
+        xa, pxa = _u32(xs, n)
+        ya, pya = _u32(ys, n)
+        vb = b"".join(int(v).to_bytes(32, "little") for v in vals)
+        out = (ctypes.c_uint8 * max(n, 1))()
+        keep = [buf(cb), buf(vb)]
+        check(self._l.hbh_bivar_ack_check(self._h, n, t, len(commits), keep[0][1], ppa, pxa, pya, keep[1][1],
+                                          ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)[:n]
+
+    # ------------------------------------------------------------ profiling
+    def set_profiling(self, on):
+        check(self._l.hbh_engine_set_profiling(self._h, 1 if on else 0))
+
+    def stage_time(self, stage):
+        """(total device ms, launches) of a stage since set_profiling."""
+        ms = ctypes.c_double()
+        nl = ctypes.c_int()
+        check(self._l.hbh_engine_stage_time(self._h, int(stage), ctypes.byref(ms), ctypes.byref(nl)))
+        return ms.value, nl.value
+
     def dbg_pairing(self, p, q):
         """e(p[i], q[i])^3 as 12 canonical Fp coefficients (LE, 48 B each) per item."""
         pb, qb = _join(p, G1_BYTES), _join(q, G2_BYTES)

@@ -95,6 +95,54 @@ int hbh_verify_pairing_eq_dev(hbh_engine* eng, void* stream, size_t n,
                               const void* d_p2, const void* d_q2_table, size_t nq2, const uint32_t* d_q2_idx,
                               uint8_t* d_verdicts);
 
+/* ---------------------------------------------------------------- combine (interpolate at 0)
+ * threshold_crypto interpolate(t, samples) for `ncomb` independent combines of exactly t+1
+ * samples each (the first t+1 of the reference's iterator, in its order): out[c] =
+ * sum_k lambda_k(0) * P[c][k] with x_k = idx[c][k] + 1.  status[c] = HBH_OK or
+ * HBH_ERR_DUPLICATE_ENTRY (two equal indices), as threshold_crypto reports it.  t = 0 returns the
+ * single sample.  A caller holding fewer than t+1 shares reports HBH_ERR_NOT_ENOUGH_SHARES itself
+ * (the reference checks that before interpolating).
+ *   PublicKeySet::combine_signatures (src/threshold_sign.rs:249-259)   -> hbh_interpolate_g2
+ *   PublicKeySet::decrypt's G1 interpolation (src/threshold_decrypt.rs:242-250; the XOR with
+ *   hash(g) stays on the host)                                         -> hbh_interpolate_g1 */
+int hbh_interpolate_g2(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out,
+                       int* status);
+int hbh_interpolate_g1(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out,
+                       int* status);
+
+/* ---------------------------------------------------------------- scalar multiplication
+ * out[i] = k_i * P_i, k_i a 32-byte little-endian integer (any value < 2^256).  Public-data helper
+ * for commitments (Poly::commitment = g1 * c_i, src/sync_key_gen.rs:508), public-key-share
+ * derivation (src/network_info.rs:59-62) and synthetic-input generation.  Secret keys stay on the
+ * host in the reference flow (sign_g2 / decrypt_share). */
+int hbh_g1_mul(hbh_engine* eng, size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out);
+int hbh_g2_mul(hbh_engine* eng, size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out);
+
+/* ---------------------------------------------------------------- SyncKeyGen commitments
+ * commits: nparts BivarCommitments of degree t, each (t+1)(t+2)/2 G1 points in threshold_crypto's
+ * coeff_pos order (j(j+1)/2 + i for i <= j).
+ * hbh_bivar_row: BivarCommitment::row(x) (src/sync_key_gen.rs:496) for nrow (part_idx, x) pairs;
+ *   out = nrow * (t+1) G1 points.  Compare with Poly::commitment (hbh_g1_mul of g1) for :508.
+ * hbh_bivar_ack_check: verdict[a] = (BivarCommitment::evaluate(x_a, y_a) == g1 * val_a)
+ *   (src/sync_key_gen.rs:542); vals are 32-byte LE Fr values (the decrypted Ack values).
+ *   x, y are the 1-based node indices the reference passes (our_idx + 1, sender_idx + 1). */
+int hbh_bivar_row(hbh_engine* eng, size_t nrow, int t, size_t nparts, const uint8_t* commits, const uint32_t* part_idx,
+                  const uint32_t* xs, uint8_t* out);
+int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, const uint8_t* commits,
+                        const uint32_t* part_idx, const uint32_t* xs, const uint32_t* ys, const uint8_t* vals,
+                        uint8_t* verdicts);
+
+/* ---------------------------------------------------------------- profiling
+ * With profiling on, the engine records HIP events around each stage's kernels on the stream they
+ * run on; hbh_engine_stage_time returns the summed device time and launch count since the last
+ * hbh_engine_set_profiling call. */
+#define HBH_STAGE_PREPARE 0 /* Miller-loop line tables (G2 walks) */
+#define HBH_STAGE_PAIRING 1 /* multi-Miller loop + final exponentiation */
+#define HBH_STAGE_CURVE 2   /* scalar multiplication / interpolation / bivariate checks */
+#define HBH_NUM_STAGES 3
+int hbh_engine_set_profiling(hbh_engine* eng, int on);
+int hbh_engine_stage_time(hbh_engine* eng, int stage, double* total_ms, int* launches);
+
 /* ---------------------------------------------------------------- debug / test entry points
  * hbh_dbg_pairing: out[i] = e(P[i], Q[i])^3 as 12 canonical Fp2 coefficients (c0.c0.c0, c0.c0.c1,
  * c0.c1.c0, ... c1.c2.c1; 48 B LE each = 576 B) -- the pairing value itself, for parity tests

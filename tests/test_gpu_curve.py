@@ -1,0 +1,138 @@
+"""GPU parity of the curve kernels (scalar multiplication, interpolate() for combine_signatures /
+threshold decryption, SyncKeyGen bivariate commitments) against the C oracle and the golden
+fixtures.  Bar: byte-identical canonical affine points, identical verdicts and statuses."""
+import json
+import os
+import random
+
+import pytest
+
+from oracle import bls12_381 as C
+from oracle import cbls, tc
+from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+G1 = g1a(C.g1_uncompressed(C.G1_GEN))
+G2 = g2a(C.g2_uncompressed(C.G2_GEN))
+EDGE_SCALARS = [0, 1, 2, 3, C.R - 1, C.R, C.R + 1, (1 << 256) - 1, 1 << 255]
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def test_g1_g2_mul(engine):
+    rng = random.Random(1)
+    ks = EDGE_SCALARS + [rng.randrange(1 << 256) for _ in range(40)]
+    p1 = [cbls.g1_mul(G1, rng.randrange(1, C.R)) for _ in range(len(ks) - 1)] + [bytes(96)]
+    assert engine.g1_mul(p1, ks) == [cbls.g1_mul(p, k) for p, k in zip(p1, ks)]
+    p2 = [cbls.g2_mul(G2, rng.randrange(1, C.R)) for _ in range(len(ks) - 1)] + [bytes(192)]
+    assert engine.g2_mul(p2, ks) == [cbls.g2_mul(p, k) for p, k in zip(p2, ks)]
+
+
+def test_combine_signatures_golden(engine):
+    d = load("threshold_sign_n10_t3.json")
+    t = d["t"]
+    for doc in d["docs"]:
+        hm = C.g2_decompress(bytes.fromhex(doc["hash_compressed"]))
+        idx = doc["combine_indices"]
+        # the valid shares of these nodes: sk_i * H, recovered from the fixture's share list
+        by_idx = {s["idx"]: s for s in doc["shares"]}
+        pts = [g2a(bytes.fromhex(by_idx[i]["sig"])) for i in idx]
+        out, st = engine.interpolate_g2(t, [idx], [pts])
+        assert st == [0]
+        assert g2a(bytes.fromhex(doc["combined_uncompressed"])) == out[0]
+        # combined signature bytes (compressed, as the reference serialises it) and coin parity
+        pt = (tuple(int.from_bytes(out[0][o:o + 48], "little") for o in (0, 48)),
+              tuple(int.from_bytes(out[0][o:o + 48], "little") for o in (96, 144)))
+        assert C.g2_compress(pt).hex() == doc["combined"]
+        assert tc.signature_parity(pt) == doc["parity"]
+        assert hm is not None
+
+
+
+def test_interpolate_g2_n64_t21_matches_oracle(engine):
+    """The BASELINE config's combine: 22 G2 shares of a degree-21 key, several index subsets."""
+    rng = random.Random(21)
+    t = 21
+    coeffs = [rng.randrange(1, C.R) for _ in range(t + 1)]
+    h = cbls.g2_mul(G2, rng.randrange(1, C.R))
+    subsets = [list(range(t + 1)), sorted(rng.sample(range(64), t + 1)), list(range(63, 63 - t - 1, -1))]
+    idx, pts = [], []
+    for sub in subsets:
+        idx.append(sub)
+        pts.append([cbls.g2_mul(h, tc.poly_eval(coeffs, i + 1)) for i in sub])
+    out, st = engine.interpolate_g2(t, idx, pts)
+    want = cbls.g2_mul(h, coeffs[0])
+    assert st == [0, 0, 0]
+    assert out == [want, want, want]
+    # same result as the reference-equivalent CPU interpolate on one subset
+    assert cbls.combine_g2(t, idx[1], pts[1]) == (0, want)
+
+
+def test_interpolate_edge_cases(engine):
+    rng = random.Random(3)
+    # t = 0 returns the sample itself
+    p = cbls.g2_mul(G2, 5)
+    out, st = engine.interpolate_g2(0, [[7]], [[p]])
+    assert st == [0] and out == [p]
+    # duplicate index -> DuplicateEntry (status 5), other combines in the batch unaffected
+    q = [cbls.g1_mul(G1, rng.randrange(1, C.R)) for _ in range(3)]
+    out, st = engine.interpolate_g1(2, [[1, 1, 2], [0, 1, 2]], [q, q])
+    assert st[0] == 5 and st[1] == 0
+    rc, want = cbls.combine_g1(2, [0, 1, 2], q)
+    assert out[1] == want
+    # shares that are the point at infinity
+    out, st = engine.interpolate_g1(1, [[0, 1]], [[bytes(96), bytes(96)]])
+    assert st == [0] and out == [bytes(96)]
+
+
+def test_threshold_decrypt_golden(engine):
+    d = load("threshold_decrypt_n10_t3.json")
+    t = d["t"]
+    for ct in d["ciphertexts"]:
+        by_idx = {s["idx"]: s for s in ct["shares"]}
+        idx = ct["combine_indices"]
+        out, st = engine.interpolate_g1(t, [idx], [[g1a(bytes.fromhex(by_idx[i]["share"])) for i in idx]])
+        assert st == [0]
+        g = (int.from_bytes(out[0][:48], "little"), int.from_bytes(out[0][48:], "little"))
+        assert tc.xor_with_hash(g, bytes.fromhex(ct["v"])) == bytes.fromhex(ct["plaintext"])
+
+
+def test_bivar_golden(engine):
+    d = load("sync_key_gen_n4_t2.json")
+    t = d["t"]
+    commit = [g1a(bytes.fromhex(h)) for h in d["commit"]]
+    rows = engine.bivar_row(t, [commit], [0] * len(d["rows"]), [r["x"] for r in d["rows"]])
+    for r, got in zip(d["rows"], rows):
+        assert got == [g1a(bytes.fromhex(h)) for h in r["row_commit"]]
+    acks = d["acks"]
+    v = engine.bivar_ack_check(t, [commit], [0] * len(acks), [a["x"] for a in acks], [a["y"] for a in acks],
+                               [int(a["val"], 16) for a in acks])
+    assert list(v) == [int(a["valid"]) for a in acks]
+
+
+def test_bivar_t33_matches_oracle(engine):
+    """SyncKeyGen N=100 t=33 shapes: 595-point commitments, rows at x = our index + 1."""
+    rng = random.Random(33)
+    t = 33
+    npos = (t + 1) * (t + 2) // 2
+    parts = []
+    polys = []
+    for _ in range(2):
+        bp = tc.BivarPoly(t, [rng.randrange(1, C.R) for _ in range(npos)])
+        polys.append(bp)
+        parts.append([cbls.g1_mul(G1, c) for c in bp.coeffs])
+    x = 17
+    rows = engine.bivar_row(t, parts, [0, 1], [x, x])
+    for bp, row in zip(polys, rows):
+        assert row == [cbls.g1_mul(G1, c) for c in bp.row(x)]
+    assert rows[0][:3] == cbls.bivar_row(t, parts[0], x)[:3]
+    ys = [1, 2, 50, 100, 7, 9]
+    pidx = [0, 1, 0, 1, 0, 1]
+    vals = [polys[p].evaluate(x, y) for p, y in zip(pidx, ys)]
+    vals[3] = (vals[3] + 1) % C.R  # a tampered Ack value
+    v = engine.bivar_ack_check(t, parts, pidx, [x] * len(ys), ys, vals)
+    assert list(v) == [1, 1, 1, 0, 1, 1]

@@ -7,8 +7,10 @@ for line in open(sys.argv[1]):
     if not line.startswith("CHECK"):
         continue
     parts = line.split()
-    name, limbs = parts[1], [int(x, 16) for x in parts[2:]]
-    w, nl = (28, 14) if name == "fips28" else (32, 12)
+    if parts[2] != "ILP1":
+        continue  # ILP>1 rows print the XOR of independent chains (keeps every chain live)
+    name, limbs = parts[1], [int(x, 16) for x in parts[3:]]
+    w, nl = (28, 14) if name in ("fips28", "os28") else (32, 12)
     a = sum(inp[j * 64 + 0] << (w * j) for j in range(nl))
     b = sum(inp[(nl + j) * 64 + 0] << (w * j) for j in range(nl))
     rinv = pow(1 << (w * nl), P - 2, P)
