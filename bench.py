@@ -129,6 +129,17 @@ def cpu_baseline(w, budget_s=12.0):
             "single_thread_value": n1 / st, "combine_latency_ms": comb_ms}
 
 
+def pmc_traffic():
+    """HBM bytes per k_pairing_eq launch from the latest committed rocprofv3 --pmc passes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/<round>/pmc_traffic.json), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
 def combine_latency(eng, w, reps=7):
     """combine_and_verify_sig for one document: interpolate the first t+1 valid shares (G2 MSM
     with Lagrange coefficients) + verify the result against the master key; host-to-host wall
@@ -165,7 +176,15 @@ def main():
     ap.add_argument("--batch", type=int, default=NDOCS * N_NODES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
+    ap.add_argument("--impl", choices=["lane_coop", "thread"], default="thread",
+                    help="pairing implementation (hbh_engine_set_pairing_impl)")
+    ap.add_argument("--workload", choices=["sign", "decrypt", "dkg"], default="sign",
+                    help="sign = BASELINE configs[1] (default, the headline metric); decrypt = configs[2] "
+                         "(64k decryption-share checks + G1 combines, strong-scaled over ranks); dkg = configs[3] "
+                         "(SyncKeyGen N=100 t=33 ack checks of one node)")
     args = ap.parse_args()
+    if args.workload != "sign":
+        return run_other(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -179,6 +198,7 @@ def main():
     from hbbft_amd._lib import STAGE_PAIRING, STAGE_PREPARE
     from hbbft_amd.engine import Engine
     eng = Engine(local)
+    eng.set_pairing_impl(1 if args.impl == "lane_coop" else 0)
     n = args.batch
     w = Workload(eng, n, seed=20261016 + rank)
 
@@ -241,11 +261,13 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
             "data": "synthetic, seeded (degree-21 key, 1024 document points, 1/64 invalid shares; generated on GPU)",
             "config": {"workload": "ThresholdSign share verification, BASELINE configs[1]", "batch_per_gpu": n,
-                       "documents_per_gpu": nh, "n_nodes": N_NODES, "f": F_FAULTY,
+                       "documents_per_gpu": nh, "n_nodes": N_NODES, "f": F_FAULTY, "pairing_impl": args.impl,
                        "parallelism": "shard-by-batch x%d" % world},
             "verdicts_ok": ok,
-            "roofline": {"bound": "valu", "kernel": "hb::k_pairing_eq", "achieved": achieved, "peak": PEAK_TMAD,
-                         "unit": "T int32-MAD/s", "frac": achieved / PEAK_TMAD, "traffic": None,
+            "roofline": {"bound": "valu",
+                         "kernel": "hbs::k_lc_* (miller+easy+exp+glue+verdict)" if args.impl == "lane_coop"
+                         else "hb::k_pairing_eq", "achieved": achieved, "peak": PEAK_TMAD,
+                         "unit": "T int32-MAD/s", "frac": achieved / PEAK_TMAD, "traffic": pmc_traffic(),
                          "kernel_ms": kern_ms, "prepare_ms": prep_ms / max(prep_n, 1),
                          "work_per_check_fpmul": fpm,
                          "note": "achieved = checks x (multi-Miller + final-exp Fp-mul) x 392 MAD / kernel time"},
@@ -257,6 +279,176 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(w)
         print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------------- other configs
+def _dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def _max_over_ranks(ms, world, dev):
+    t = torch.tensor([ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_decrypt(args, eng, world, rank, dev):
+    """configs[2]: 65,536 decryption-share checks e(D_i, H_uv) == e(pk_i, W) over 1,024 ciphertexts
+    (src/threshold_decrypt.rs:227) + one G1 interpolation per ciphertext (:249); the whole batch is
+    fixed and split over the ranks by ciphertext (hbbft_amd/shard.py) -> strong scaling."""
+    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
+    from hbbft_amd.shard import shard_by_instance
+    rng = random.Random(4242)
+    g1, g2 = g1a(G1_UNC), g2a(G2_UNC)
+    ncts, total = NDOCS, NDOCS * N_NODES
+    inst = np.arange(total) // N_NODES
+    lo, hi = shard_by_instance(total, inst, rank, world)
+    clo, chi = int(inst[lo]) if hi > lo else 0, int(inst[hi - 1]) + 1 if hi > lo else 0
+    coeffs = [rng.randrange(1, R_ORDER) for _ in range(T + 1)]
+    sk = [poly_eval(coeffs, i + 1) for i in range(N_NODES)]
+    pks = eng.g1_mul([g1] * N_NODES, sk)
+    rs = [rng.randrange(1, R_ORDER) for _ in range(ncts)]
+    hs = [rng.randrange(1, R_ORDER) for _ in range(ncts)]
+    mine = list(range(clo, chi))
+    us = eng.g1_mul([g1] * len(mine), [rs[c] for c in mine])                        # U = g1 r
+    huv = eng.g2_mul([g2] * len(mine), [hs[c] for c in mine])                       # H_uv (synthetic hash)
+    ws = eng.g2_mul([g2] * len(mine), [hs[c] * rs[c] % R_ORDER for c in mine])      # W = H_uv r
+    bad = {c * N_NODES + (c * 29) % N_NODES for c in mine}
+    items = list(range(lo, hi))
+    shares = eng.g1_mul([us[inst[i] - clo] for i in items],
+                        [(rng.randrange(1, R_ORDER) if i in bad else sk[i % N_NODES]) for i in items])
+    expected = np.array([0 if i in bad else 1 for i in items], dtype=np.uint8)
+    n = len(items)
+    to_dev = lambda b: torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).to(dev)  # noqa: E731
+    d_d = to_dev(b"".join(shares))
+    d_pk = to_dev(b"".join(pks[i % N_NODES] for i in items))
+    d_h = to_dev(b"".join(huv))
+    d_w = to_dev(b"".join(ws))
+    d_ci = torch.from_numpy((inst[lo:hi] - clo).astype(np.int32)).to(dev)
+    d_v = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+    ts = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        eng.verify_pairing_eq_dev(ts.cuda_stream, n, d_d.data_ptr(), d_h.data_ptr(), len(mine), d_ci.data_ptr(),
+                                  d_pk.data_ptr(), d_w.data_ptr(), len(mine), d_ci.data_ptr(), d_v.data_ptr())
+
+    step()
+    torch.cuda.synchronize(dev)
+    ok = bool((d_v.cpu().numpy()[:n] == expected).all())
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(ts)
+    for _ in range(args.steps):
+        step()
+    ev1.record(ts)
+    torch.cuda.synchronize(dev)
+    ms_step = _max_over_ranks(ev0.elapsed_time(ev1), world, dev) / args.steps
+    # combines: first t+1 valid shares per ciphertext -> g = U * msk
+    cidx, cpts = [], []
+    for j, c in enumerate(mine):
+        ids = [k for k in range(N_NODES) if expected[(c - clo) * N_NODES + k]][: T + 1]
+        cidx.append(ids)
+        cpts.append([shares[(c - clo) * N_NODES + k] for k in ids])
+    t0 = time.perf_counter()
+    out, st = eng.interpolate_g1(T, cidx, cpts)
+    comb_s = time.perf_counter() - t0
+    want = eng.g1_mul(us, [coeffs[0]] * len(mine))
+    ok = ok and out == want and all(x == 0 for x in st)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "verified decryption shares/sec (whole node), N=64 f=21", "value": total / (ms_step / 1e3),
+            "unit": "shares/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
+            "data": "synthetic, seeded (H_uv synthetic in G2; 1/64 invalid shares)",
+            "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total,
+                       "ciphertexts": ncts, "parallelism": "shard-by-ciphertext x%d" % world},
+            "verdicts_ok": ok, "combines_per_s_rank0": len(mine) / comb_s}), flush=True)
+
+
+def run_dkg(args, eng, world, rank, dev):
+    """configs[3]: SyncKeyGen N=100 t=33 -- the 10,000 Ack checks of one node
+    (BivarCommitment::evaluate == g1*val, src/sync_key_gen.rs:542) over 100 Parts with 595-point
+    commitments; ranks split the checks by Part (weak scaling: every rank plays one node)."""
+    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
+    rng = random.Random(100 + rank)
+    n_nodes, t = 100, 33
+    npos = (t + 1) * (t + 2) // 2
+    g1 = g1a(G1_UNC)
+    parts = []
+    coefs = []
+    for _ in range(n_nodes):
+        c = [rng.randrange(1, R_ORDER) for _ in range(npos)]
+        coefs.append(c)
+    flat = eng.g1_mul([g1] * (n_nodes * npos), [x for c in coefs for x in c])
+    parts = [flat[p * npos:(p + 1) * npos] for p in range(n_nodes)]
+    x = rank + 1
+    pidx, xs, ys, vals = [], [], [], []
+
+    def cp(i, j):
+        return j * (j + 1) // 2 + i if i <= j else i * (i + 1) // 2 + j
+
+    for p in range(n_nodes):
+        xp = [pow(x, i, R_ORDER) for i in range(t + 1)]
+        row = [sum(coefs[p][cp(i, j)] * xp[i] for i in range(t + 1)) % R_ORDER for j in range(t + 1)]
+        for y in range(1, n_nodes + 1):
+            v = 0
+            for j in reversed(range(t + 1)):
+                v = (v * y + row[j]) % R_ORDER
+            pidx.append(p)
+            xs.append(x)
+            ys.append(y)
+            vals.append(v)
+    bad = set(range(0, len(vals), 97))
+    for a in bad:
+        vals[a] = (vals[a] + 1) % R_ORDER
+    expected = bytes(0 if a in bad else 1 for a in range(len(vals)))
+    v = eng.bivar_ack_check(t, parts, pidx, xs, ys, vals)
+    ok = v == expected
+    if world > 1:
+        dist.barrier()
+    times = []
+    for _ in range(max(1, args.steps // 5)):
+        t0 = time.perf_counter()
+        v = eng.bivar_ack_check(t, parts, pidx, xs, ys, vals)
+        times.append((time.perf_counter() - t0) * 1e3)
+    ok = ok and v == expected
+    ms = _max_over_ranks(statistics.median(times), world, dev)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SyncKeyGen ack checks/sec (whole node set), N=100 t=33", "value": len(vals) * world / (ms / 1e3),
+            "unit": "acks/s", "n_gpus": world, "steps": len(times), "warmup": 1, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
+            "data": "synthetic, seeded (100 random degree-33 bivariate polynomials; 1/97 tampered values)",
+            "config": {"workload": "SyncKeyGen ack checks of one node, BASELINE configs[3]", "acks_per_rank": len(vals),
+                       "parts": n_nodes, "commitment_points": npos, "parallelism": "one node per rank x%d" % world,
+                       "timing": "host-to-host through the C ABI (commitments, values and verdicts cross PCIe)"},
+            "verdicts_ok": ok}), flush=True)
+
+
+def run_other(args):
+    world, rank, local = _dist_env()
+    dev = torch.device("cuda", local)
+    from hbbft_amd.engine import Engine
+    eng = Engine(local)
+    if args.workload == "decrypt":
+        run_decrypt(args, eng, world, rank, dev)
+    else:
+        run_dkg(args, eng, world, rank, dev)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhbbft_hip.so")
+# HBBFT_HIP_LIB overrides the in-tree library (A/B builds of the same sources)
+LIB_PATH = os.environ.get("HBBFT_HIP_LIB") or os.path.join(_HERE, "libhbbft_hip.so")
 
 G1_BYTES = 96
 G2_BYTES = 192
@@ -35,10 +36,12 @@ SIGNATURES = [
     ("hbh_g2_mul", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_bivar_row", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),
     ("hbh_bivar_ack_check", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P, _P, _P]),
+    ("hbh_engine_set_pairing_impl", _I, [_P, _I]),
     ("hbh_engine_set_profiling", _I, [_P, _I]),
     ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
+IMPL_THREAD, IMPL_LANE_COOP = 0, 1
 
 _lib = None
 

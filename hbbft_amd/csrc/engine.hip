@@ -83,9 +83,10 @@ struct hbh_engine {
   hipStream_t stream = nullptr;
   std::mutex mu;
   bool profiling = false;
+  int impl = HBH_IMPL_THREAD;  // pairing implementation (hbh_engine_set_pairing_impl); faster on MI355X today
   StageTimer timer;
   // workspaces
-  DevBuf coef1, coef2, inf1, inf2, work, status;
+  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3;
   // staging for host-pointer entry points
   DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
 };
@@ -113,6 +114,9 @@ int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, 
   return HBH_OK;
 }
 
+int launch_pairing(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, size_t nq1, const uint32_t* d_i1,
+                   const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v, uint32_t* d_value);
+
 int run_pairing_eq_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
                        const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2,
                        uint8_t* d_v) {
@@ -120,9 +124,25 @@ int run_pairing_eq_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1,
   if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
   int rc = launch_prepare(e, s, d_q1, nq1, e->coef1, e->inf1, d_q2, nq2, &e->coef2, &e->inf2);
   if (rc) return rc;
+  return launch_pairing(e, s, n, d_p1, nq1, d_i1, d_p2, nq2, d_i2, 1, d_v, nullptr);
+}
+
+// multi-Miller loop + final exponentiation over prepared tables (coef1/2, inf1/2)
+int launch_pairing(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, size_t nq1, const uint32_t* d_i1,
+                   const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v, uint32_t* d_value) {
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  HBH_CHECK(hbl::pairing_eq(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2, e->coef2.p,
-                            (int)nq2, (const uint8_t*)e->inf2.p, d_i2, d_v));
+  if (e->impl == HBH_IMPL_LANE_COOP) {
+    const size_t bytes = hbl::lc_state_words((int)n) * sizeof(int32_t);
+    for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
+    HBH_CHECK(hbl::lc_pairing(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
+                              e->coef2.p, (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, (int32_t*)e->lc0.p,
+                              (int32_t*)e->lc1.p, (int32_t*)e->lc2.p, (int32_t*)e->lc3.p, d_v, d_value));
+  } else if (d_value) {
+    HBH_CHECK(hbl::pairing_value(s, (int)n, d_p1, e->coef1.p, (const uint8_t*)e->inf1.p, d_value));
+  } else {
+    HBH_CHECK(hbl::pairing_eq(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
+                              e->coef2.p, (int)nq2, (const uint8_t*)e->inf2.p, d_i2, d_v));
+  }
   e->timer.end(s, t);
   return HBH_OK;
 }
@@ -230,7 +250,8 @@ int hbh_engine_destroy(hbh_engine* e) {
   (void)hipSetDevice(e->device);
   (void)hipStreamSynchronize(e->stream);
   e->timer.clear();
-  for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->in_p1, &e->in_q1, &e->in_i1,
+  for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->lc0, &e->lc1, &e->lc2, &e->lc3,
+                    &e->in_p1, &e->in_q1, &e->in_i1,
                     &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v, &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x})
     b->release();
   (void)hipStreamDestroy(e->stream);
@@ -299,11 +320,21 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
   HBH_CHECK(e->out_v.ensure(n * 576));
   HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p, n * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_q1.p, q, n * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
-  int rc = launch_prepare(e, s, e->in_q1.p, n, e->coef1, e->inf1);
+  HBH_CHECK(e->in_p2.ensure(n * HBH_G1_BYTES));
+  HBH_CHECK(hipMemsetAsync(e->in_p2.p, 0, n * HBH_G1_BYTES, s));  // second pair inactive (P2 = O)
+  int rc = launch_prepare(e, s, e->in_q1.p, n, e->coef1, e->inf1, e->in_q1.p, n, &e->coef2, &e->inf2);
   if (rc) return rc;
-  HBH_CHECK(hbl::pairing_value(s, (int)n, e->in_p1.p, e->coef1.p, (const uint8_t*)e->inf1.p, (uint32_t*)e->out_v.p));
+  rc = launch_pairing(e, s, n, e->in_p1.p, n, nullptr, e->in_p2.p, n, nullptr, 2, nullptr, (uint32_t*)e->out_v.p);
+  if (rc) return rc;
   HBH_CHECK(hipMemcpyAsync(out, e->out_v.p, n * 576, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
+  if (!e || (impl != HBH_IMPL_THREAD && impl != HBH_IMPL_LANE_COOP)) return fail(HBH_ERR_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->impl = impl;
   return HBH_OK;
 }
 

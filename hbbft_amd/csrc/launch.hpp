@@ -25,6 +25,16 @@ hipError_t pairing_eq(hipStream_t s, int n, const void* p1, const void* coef1, i
 // out[i] = e(P_i, Q_i)^3 as 144 canonical words (debug / parity).
 hipError_t pairing_value(hipStream_t s, int n, const void* p, const void* coef, const uint8_t* inf, uint32_t* out);
 
+// --------------------------------------------------------------- lane-cooperative pairing (k_lc.hip)
+// The same verdicts as pairing_eq (or, with value_out, e(P1,Q1)^3 e(P2,Q2)^3 words when flags has
+// bit 2 set and P2 = O), six lanes per check; w0..w3 are scratch of lc_state_words(n) int32 each.
+size_t lc_lstride(int n);
+size_t lc_state_words(int n);
+hipError_t lc_pairing(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
+                      const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,
+                      const uint32_t* idx2, int flags, int32_t* w0, int32_t* w1, int32_t* w2, int32_t* w3,
+                      uint8_t* verdict, uint32_t* value_out);
+
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).
 hipError_t g1_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars, void* out);

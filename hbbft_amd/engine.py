@@ -186,6 +186,10 @@ class Engine:
                                           ctypes.cast(out, ctypes.c_void_p)))
         return bytes(out)[:n]
 
+    def set_pairing_impl(self, impl):
+        """0 = one thread per check (default), 1 = lane-cooperative (six lanes per check)."""
+        check(self._l.hbh_engine_set_pairing_impl(self._h, int(impl)))
+
     # ------------------------------------------------------------ profiling
     def set_profiling(self, on):
         check(self._l.hbh_engine_set_profiling(self._h, 1 if on else 0))

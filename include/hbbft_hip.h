@@ -132,6 +132,15 @@ int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, cons
                         const uint32_t* part_idx, const uint32_t* xs, const uint32_t* ys, const uint8_t* vals,
                         uint8_t* verdicts);
 
+/* ---------------------------------------------------------------- implementation selection
+ * Two pairing implementations with identical verdicts: HBH_IMPL_THREAD (default: one thread per
+ * check, 37.6 ms per 65,536 checks on MI355X) and HBH_IMPL_LANE_COOP (six lanes per check, one Fp2
+ * coefficient of the Fp12 accumulator per lane; 47 ms today).  Selectable for A/B measurement and
+ * cross-checking. */
+#define HBH_IMPL_THREAD 0
+#define HBH_IMPL_LANE_COOP 1
+int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
+
 /* ---------------------------------------------------------------- profiling
  * With profiling on, the engine records HIP events around each stage's kernels on the stream they
  * run on; hbh_engine_stage_time returns the summed device time and launch count since the last

@@ -13,6 +13,14 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
+@pytest.fixture(params=[1, 0], ids=["lane_coop", "thread"])
+def eng(engine, request):
+    """Both pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD) must give identical results."""
+    engine.set_pairing_impl(request.param)
+    yield engine
+    engine.set_pairing_impl(0)
+
+
 def load(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)
@@ -22,17 +30,17 @@ def f12_bytes(e):
     return b"".join(c.to_bytes(48, "little") for six in e for f2 in six for c in f2)
 
 
-def test_pairing_value_matches_oracle(engine):
+def test_pairing_value_matches_oracle(eng):
     P = [C.g1_mul(C.G1_GEN, k) for k in (1, 5, 12345)]
     Q = [C.g2_mul(C.G2_GEN, k) for k in (1, 7, 999)]
-    out = engine.dbg_pairing([g1a(C.g1_uncompressed(p)) for p in P], [g2a(C.g2_uncompressed(q)) for q in Q])
+    out = eng.dbg_pairing([g1a(C.g1_uncompressed(p)) for p in P], [g2a(C.g2_uncompressed(q)) for q in Q])
     for k, (p, q) in enumerate(zip(P, Q)):
         assert out[k] == f12_bytes(C.f12_pow(C.pairing(p, q), 3)), k
 
 
-def test_pairing_with_infinity_is_one(engine):
+def test_pairing_with_infinity_is_one(eng):
     one = f12_bytes(C.F12_ONE)
-    out = engine.dbg_pairing([bytes(96), g1a(C.g1_uncompressed(C.G1_GEN))],
+    out = eng.dbg_pairing([bytes(96), g1a(C.g1_uncompressed(C.G1_GEN))],
                              [g2a(C.g2_uncompressed(C.G2_GEN)), bytes(192)])
     assert out == [one, one]
 
@@ -49,21 +57,21 @@ def sign_batch(d):
     return pks, sigs, hashes, didx, exp
 
 
-def test_sig_share_verdicts_golden(engine):
+def test_sig_share_verdicts_golden(eng):
     pks, sigs, hashes, didx, exp = sign_batch(load("threshold_sign_n10_t3.json"))
-    assert list(engine.verify_sig_shares(pks, sigs, hashes, didx)) == exp
+    assert list(eng.verify_sig_shares(pks, sigs, hashes, didx)) == exp
 
 
-def test_sig_share_verdicts_golden_tiled(engine):
+def test_sig_share_verdicts_golden_tiled(eng):
     """Ragged batch (not a multiple of the workgroup) with shuffled document indices."""
     pks, sigs, hashes, didx, exp = sign_batch(load("threshold_sign_n10_t3.json"))
     reps = 13
     order = [(i * 7 + r) % len(pks) for r in range(reps) for i in range(len(pks))]
-    v = engine.verify_sig_shares([pks[i] for i in order], [sigs[i] for i in order], hashes, [didx[i] for i in order])
+    v = eng.verify_sig_shares([pks[i] for i in order], [sigs[i] for i in order], hashes, [didx[i] for i in order])
     assert list(v) == [exp[i] for i in order]
 
 
-def test_dec_share_and_ciphertext_verdicts_golden(engine):
+def test_dec_share_and_ciphertext_verdicts_golden(eng):
     d = load("threshold_decrypt_n10_t3.json")
     shares, pks, huv, w, cidx, exp = [], [], [], [], [], []
     for ci, ct in enumerate(d["ciphertexts"]):
@@ -74,11 +82,47 @@ def test_dec_share_and_ciphertext_verdicts_golden(engine):
             pks.append(g1a(bytes.fromhex(d["pk_shares"][s["idx"]])))
             cidx.append(ci)
             exp.append(int(s["valid"]))
-    assert list(engine.verify_dec_shares(shares, pks, huv, w, cidx)) == exp
+    assert list(eng.verify_dec_shares(shares, pks, huv, w, cidx)) == exp
     u = [g1a(bytes.fromhex(ct["u"])) for ct in d["ciphertexts"]]
     bad_w = [g2a(bytes.fromhex(ct["bad_w"])) for ct in d["ciphertexts"]]
-    assert list(engine.verify_ciphertexts(u + u, w + bad_w, huv + huv)) == [1, 1, 0, 0]
+    assert list(eng.verify_ciphertexts(u + u, w + bad_w, huv + huv)) == [1, 1, 0, 0]
 
 
-def test_empty_batch(engine):
-    assert engine.verify_sig_shares(b"", b"", bytes(192), None) == b""
+def test_empty_batch(eng):
+    assert eng.verify_sig_shares(b"", b"", bytes(192), None) == b""
+
+
+def test_lane_coop_matches_thread_random_batch(engine):
+    """A 1,000-check random batch (valid, swapped, infinity, ragged vs the 10-checks-per-wave
+    lane-cooperative layout): both implementations and the C oracle agree on every verdict."""
+    import random
+    from oracle import cbls
+    rng = random.Random(7)
+    g1, g2 = g1a(C.g1_uncompressed(C.G1_GEN)), g2a(C.g2_uncompressed(C.G2_GEN))
+    hs = [cbls.g2_mul(g2, rng.randrange(1, C.R)) for _ in range(3)]
+    sk = [rng.randrange(1, C.R) for _ in range(7)]
+    pks = [cbls.g1_mul(g1, k) for k in sk]
+    n = 1003
+    P, S, D, want = [], [], [], []
+    for i in range(n):
+        d, j = i % 3, i % 7
+        kind = i % 11
+        pk, sig = pks[j], cbls.g2_mul(hs[d], sk[j])
+        if kind == 3:
+            sig = cbls.g2_mul(hs[(d + 1) % 3], sk[j])
+        elif kind == 5:
+            pk = pks[(j + 1) % 7]
+        elif kind == 7:
+            pk, sig = bytes(96), bytes(192)
+        P.append(pk), S.append(sig), D.append(d)
+    for i in range(0, n, 97):
+        want.append((i, cbls.verify_g2(P[i], S[i], hs[D[i]])))
+    engine.set_pairing_impl(1)
+    v1 = engine.verify_sig_shares(P, S, hs, D)
+    engine.set_pairing_impl(0)
+    v0 = engine.verify_sig_shares(P, S, hs, D)
+    engine.set_pairing_impl(0)
+    assert v1 == v0
+    for i, w in want:
+        assert v1[i] == int(w), i
+    assert sum(v1) == sum(1 for i in range(n) if i % 11 not in (3, 5))
