@@ -38,6 +38,10 @@ METRIC = "verified BLS sig shares/sec (whole node) + combine latency, N=64 f=21"
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 MADS_PER_FPMUL = 2 * 14 * 14          # 14 x 28-bit limbs: product + Montgomery reduction
 PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # v_mad_u64_u32 at half rate: 256 CU x 4 SIMD32 x 2.4 GHz
+IMPLS = {"thread": 0, "lane_coop": 1, "thread_signed": 2}   # HBH_IMPL_* (include/hbbft_hip.h)
+KERNEL_NAMES = {"thread": "hb::k_pairing_eq",
+                "lane_coop": "hbs::k_lc_* (miller+easy+exp+glue+verdict)",
+                "thread_signed": "hbs::k_ts_* (miller+easy+exp+glue+verdict)"}
 G1_UNC = bytes.fromhex(
     "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
     "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
@@ -176,7 +180,7 @@ def main():
     ap.add_argument("--batch", type=int, default=NDOCS * N_NODES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
-    ap.add_argument("--impl", choices=["lane_coop", "thread"], default="thread",
+    ap.add_argument("--impl", choices=["lane_coop", "thread", "thread_signed"], default="thread",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--workload", choices=["sign", "decrypt", "dkg"], default="sign",
                     help="sign = BASELINE configs[1] (default, the headline metric); decrypt = configs[2] "
@@ -198,7 +202,7 @@ def main():
     from hbbft_amd._lib import STAGE_PAIRING, STAGE_PREPARE
     from hbbft_amd.engine import Engine
     eng = Engine(local)
-    eng.set_pairing_impl(1 if args.impl == "lane_coop" else 0)
+    eng.set_pairing_impl(IMPLS[args.impl])
     n = args.batch
     w = Workload(eng, n, seed=20261016 + rank)
 
@@ -265,8 +269,7 @@ def main():
                        "parallelism": "shard-by-batch x%d" % world},
             "verdicts_ok": ok,
             "roofline": {"bound": "valu",
-                         "kernel": "hbs::k_lc_* (miller+easy+exp+glue+verdict)" if args.impl == "lane_coop"
-                         else "hb::k_pairing_eq", "achieved": achieved, "peak": PEAK_TMAD,
+                         "kernel": KERNEL_NAMES[args.impl], "achieved": achieved, "peak": PEAK_TMAD,
                          "unit": "T int32-MAD/s", "frac": achieved / PEAK_TMAD, "traffic": pmc_traffic(),
                          "kernel_ms": kern_ms, "prepare_ms": prep_ms / max(prep_n, 1),
                          "work_per_check_fpmul": fpm,

@@ -131,7 +131,13 @@ int run_pairing_eq_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1,
 int launch_pairing(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, size_t nq1, const uint32_t* d_i1,
                    const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v, uint32_t* d_value) {
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  if (e->impl == HBH_IMPL_LANE_COOP) {
+  if (e->impl == HBH_IMPL_THREAD_SIGNED) {
+    const size_t bytes = hbl::ts_state_bytes((int)n);
+    for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
+    HBH_CHECK(hbl::ts_miller(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2, e->coef2.p,
+                             (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, e->lc0.p));
+    HBH_CHECK(hbl::ts_final_exp(s, (int)n, e->lc0.p, e->lc1.p, e->lc2.p, e->lc3.p, d_v, d_value));
+  } else if (e->impl == HBH_IMPL_LANE_COOP) {
     const size_t bytes = hbl::lc_state_words((int)n) * sizeof(int32_t);
     for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
     HBH_CHECK(hbl::lc_pairing(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
@@ -332,7 +338,7 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 }
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
-  if (!e || (impl != HBH_IMPL_THREAD && impl != HBH_IMPL_LANE_COOP)) return fail(HBH_ERR_ARG, "bad argument");
+  if (!e || (impl != HBH_IMPL_THREAD && impl != HBH_IMPL_LANE_COOP && impl != HBH_IMPL_THREAD_SIGNED)) return fail(HBH_ERR_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;
   return HBH_OK;

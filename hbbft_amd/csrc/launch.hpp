@@ -35,6 +35,16 @@ hipError_t lc_pairing(hipStream_t s, int n, const void* p1, const void* coef1, i
                       const uint32_t* idx2, int flags, int32_t* w0, int32_t* w1, int32_t* w2, int32_t* w3,
                       uint8_t* verdict, uint32_t* value_out);
 
+// --------------------------------------------------------------- signed thread pairing (k_ts_*.hip)
+// The same verdicts / values as lc_pairing, one thread per check on signed limbs.  w0..w3 are
+// scratch of ts_state_bytes(n) each (the Fp12 state handed between stage kernels).
+size_t ts_state_bytes(int n);
+hipError_t ts_miller(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
+                     const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,
+                     const uint32_t* idx2, int flags, void* w0);
+hipError_t ts_final_exp(hipStream_t s, int n, void* w0, void* w1, void* w2, void* w3, uint8_t* verdict,
+                        uint32_t* value_out);
+
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).
 hipError_t g1_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars, void* out);

@@ -24,6 +24,13 @@
 #define HS_HD inline
 #endif
 
+// fp_mul / fp_sqr linkage: inlined by default (lane-cooperative kernels); a translation unit may
+// define HS_MULFN as a static non-inlined device function to keep one copy hot in the
+// instruction cache (the one-thread-per-check kernel of k_thread.hip).
+#ifndef HS_MULFN
+#define HS_MULFN HS_HD
+#endif
+
 namespace hbs {
 
 using hb::NL;
@@ -58,7 +65,7 @@ HS_HD Fp fp_one() { return fp_const(hb::ONE_L); }
 
 // Product scanning (FIPS): column k accumulates a_i b_{k-i} and m_i p_{k-i} in one int64; m_k
 // clears the low 28 bits, the arithmetic shift then carries exactly (also for negative sums).
-HS_HD Fp fp_mul(const Fp& a, const Fp& b) {
+HS_MULFN Fp fp_mul(Fp a, Fp b) {
   int32_t m[NL];
   int64_t acc = 0;
   Fp r;
@@ -86,7 +93,7 @@ HS_HD Fp fp_mul(const Fp& a, const Fp& b) {
   return r;
 }
 
-HS_HD Fp fp_sqr(const Fp& a) {
+HS_MULFN Fp fp_sqr(Fp a) {
   int32_t m[NL];
   int64_t acc = 0;
   Fp r;

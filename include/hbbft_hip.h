@@ -139,6 +139,7 @@ int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, cons
  * cross-checking. */
 #define HBH_IMPL_THREAD 0
 #define HBH_IMPL_LANE_COOP 1
+#define HBH_IMPL_THREAD_SIGNED 2 /* one thread per check on signed limbs, stage kernels (k_ts_*.hip) */
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 
 /* ---------------------------------------------------------------- profiling

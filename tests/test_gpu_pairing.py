@@ -13,9 +13,10 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[1, 0], ids=["lane_coop", "thread"])
+@pytest.fixture(params=[1, 2, 0], ids=["lane_coop", "thread_signed", "thread"])
 def eng(engine, request):
-    """Both pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD) must give identical results."""
+    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_THREAD) must
+    give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine
     engine.set_pairing_impl(0)
@@ -94,7 +95,7 @@ def test_empty_batch(eng):
 
 def test_lane_coop_matches_thread_random_batch(engine):
     """A 1,000-check random batch (valid, swapped, infinity, ragged vs the 10-checks-per-wave
-    lane-cooperative layout): both implementations and the C oracle agree on every verdict."""
+    lane-cooperative layout): all implementations and the C oracle agree on every verdict."""
     import random
     from oracle import cbls
     rng = random.Random(7)
@@ -119,10 +120,12 @@ def test_lane_coop_matches_thread_random_batch(engine):
         want.append((i, cbls.verify_g2(P[i], S[i], hs[D[i]])))
     engine.set_pairing_impl(1)
     v1 = engine.verify_sig_shares(P, S, hs, D)
+    engine.set_pairing_impl(2)
+    v2 = engine.verify_sig_shares(P, S, hs, D)
     engine.set_pairing_impl(0)
     v0 = engine.verify_sig_shares(P, S, hs, D)
-    engine.set_pairing_impl(0)
     assert v1 == v0
+    assert v2 == v0
     for i, w in want:
         assert v1[i] == int(w), i
     assert sum(v1) == sum(1 for i in range(n) if i % 11 not in (3, 5))
