@@ -65,7 +65,17 @@ HS_HD Fp fp_one() { return fp_const(hb::ONE_L); }
 
 // Product scanning (FIPS): column k accumulates a_i b_{k-i} and m_i p_{k-i} in one int64; m_k
 // clears the low 28 bits, the arithmetic shift then carries exactly (also for negative sums).
-HS_MULFN Fp fp_mul(Fp a, Fp b) {
+// The multiplier takes its operands as 28 scalar arguments: the AMDGPU calling convention passes
+// scalars in VGPRs v0-v31, but an aggregate (struct Fp) beyond 16 argument registers through the
+// stack -- a 56-byte scratch store + load per call when HS_MULFN is a real call.
+#define HS_L14(p) p##0, p##1, p##2, p##3, p##4, p##5, p##6, p##7, p##8, p##9, p##10, p##11, p##12, p##13
+#define HS_P14(p) int32_t p##0, int32_t p##1, int32_t p##2, int32_t p##3, int32_t p##4, int32_t p##5, int32_t p##6, \
+                  int32_t p##7, int32_t p##8, int32_t p##9, int32_t p##10, int32_t p##11, int32_t p##12, int32_t p##13
+#define HS_E14(x) x.l[0], x.l[1], x.l[2], x.l[3], x.l[4], x.l[5], x.l[6], x.l[7], x.l[8], x.l[9], x.l[10], x.l[11], x.l[12], x.l[13]
+
+HS_MULFN Fp fp_mul_l(HS_P14(x), HS_P14(y)) {
+  const Fp a = {{HS_L14(x)}};
+  const Fp b = {{HS_L14(y)}};
   int32_t m[NL];
   int64_t acc = 0;
   Fp r;
@@ -93,7 +103,8 @@ HS_MULFN Fp fp_mul(Fp a, Fp b) {
   return r;
 }
 
-HS_MULFN Fp fp_sqr(Fp a) {
+HS_MULFN Fp fp_sqr_l(HS_P14(x)) {
+  const Fp a = {{HS_L14(x)}};
   int32_t m[NL];
   int64_t acc = 0;
   Fp r;
@@ -125,6 +136,9 @@ HS_MULFN Fp fp_sqr(Fp a) {
   r.l[NL - 1] = (int32_t)acc;
   return r;
 }
+
+HS_HD Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_l(HS_E14(a), HS_E14(b)); }
+HS_HD Fp fp_sqr(const Fp& a) { return fp_sqr_l(HS_E14(a)); }
 
 HS_HD void fp_norm(Fp& a) {
 #pragma unroll

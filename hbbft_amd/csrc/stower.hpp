@@ -88,9 +88,12 @@ HS_HD Fp12 f12_sqr(const Fp12& a) {
 }
 // f (c0 + c1 w^2 + c4 w^3); c0, c1, c4 < 2p
 HS_HD Fp12 f12_mul_014(const Fp12& f, const Fp2& c0, const Fp2& c1, const Fp2& c4) {
+  // sums first: f.c0 and f.c1 then die at their last product (lower peak register pressure)
+  const Fp6 fs = f6_add(f.c0, f.c1);
+  const Fp2 c14 = f2_add(c1, c4);
   const Fp6 t0 = f6_red(f6_mul_01(f.c0, c0, c1));
   const Fp6 t1 = f6_red(f6_mul_1(f.c1, c4));
-  const Fp6 s = f6_red(f6_mul_01(f6_add(f.c0, f.c1), c0, f2_add(c1, c4)));
+  const Fp6 s = f6_red(f6_mul_01(fs, c0, c14));
   return f12_red({f6_add(t0, f6_mul_v(t1)), f6_sub(f6_sub(s, t0), t1)});
 }
 HS_HD Fp12 f12_inv(const Fp12& a) {
