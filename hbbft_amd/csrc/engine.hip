@@ -83,7 +83,7 @@ struct hbh_engine {
   hipStream_t stream = nullptr;
   std::mutex mu;
   bool profiling = false;
-  int impl = HBH_IMPL_THREAD;  // pairing implementation (hbh_engine_set_pairing_impl); faster on MI355X today
+  int impl = HBH_IMPL_AUTO;  // pairing implementation (hbh_engine_set_pairing_impl)
   StageTimer timer;
   // workspaces
   DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3;
@@ -131,13 +131,15 @@ int run_pairing_eq_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1,
 int launch_pairing(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, size_t nq1, const uint32_t* d_i1,
                    const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v, uint32_t* d_value) {
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  if (e->impl == HBH_IMPL_THREAD_SIGNED) {
+  int impl = e->impl;
+  if (impl == HBH_IMPL_AUTO) impl = n < HBH_AUTO_LANE_COOP_MAX ? HBH_IMPL_LANE_COOP : HBH_IMPL_THREAD_SIGNED;
+  if (impl == HBH_IMPL_THREAD_SIGNED) {
     const size_t bytes = hbl::ts_state_bytes((int)n);
     for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
     HBH_CHECK(hbl::ts_miller(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2, e->coef2.p,
                              (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, e->lc0.p));
     HBH_CHECK(hbl::ts_final_exp(s, (int)n, e->lc0.p, e->lc1.p, e->lc2.p, e->lc3.p, d_v, d_value));
-  } else if (e->impl == HBH_IMPL_LANE_COOP) {
+  } else if (impl == HBH_IMPL_LANE_COOP) {
     const size_t bytes = hbl::lc_state_words((int)n) * sizeof(int32_t);
     for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
     HBH_CHECK(hbl::lc_pairing(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
@@ -338,7 +340,7 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 }
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
-  if (!e || (impl != HBH_IMPL_THREAD && impl != HBH_IMPL_LANE_COOP && impl != HBH_IMPL_THREAD_SIGNED)) return fail(HBH_ERR_ARG, "bad argument");
+  if (!e || impl < HBH_IMPL_THREAD || impl > HBH_IMPL_AUTO) return fail(HBH_ERR_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;
   return HBH_OK;
@@ -421,16 +423,15 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
   HBH_CHECK(e->in_b.ensure(ncomb * m * pb));
   HBH_CHECK(e->out_x.ensure(ncomb * pb));
   HBH_CHECK(e->status.ensure(ncomb * sizeof(int)));
-  HBH_CHECK(e->work.ensure(hbl::combine_work_bytes((int)ncomb, (int)m, g2)));
   HBH_CHECK(hipMemcpyAsync(e->in_a.p, xs.data(), ncomb * m * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_b.p, pts, ncomb * m * pb, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
   if (g2)
-    HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->work.p, e->out_x.p,
+    HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
                               (int*)e->status.p));
   else
-    HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->work.p, e->out_x.p,
+    HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
                               (int*)e->status.p));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * pb, hipMemcpyDeviceToHost, s));

@@ -61,8 +61,20 @@ HB_HD Fp fp_zero() {
 
 HB_HD Fp fp_one() { return fp_const(ONE_L); }
 
+// The non-inlined products take their operands as 14 scalar arguments each: the AMDGPU calling
+// convention passes scalars in VGPRs v0-v31 but an aggregate (struct Fp) beyond 16 argument
+// registers through the stack, i.e. a scratch store + load of 56 B per operand per call.
+#define HB_L14(p) p##0, p##1, p##2, p##3, p##4, p##5, p##6, p##7, p##8, p##9, p##10, p##11, p##12, p##13
+#define HB_P14(p) uint32_t p##0, uint32_t p##1, uint32_t p##2, uint32_t p##3, uint32_t p##4, uint32_t p##5, \
+                  uint32_t p##6, uint32_t p##7, uint32_t p##8, uint32_t p##9, uint32_t p##10, uint32_t p##11, \
+                  uint32_t p##12, uint32_t p##13
+#define HB_E14(x) x.l[0], x.l[1], x.l[2], x.l[3], x.l[4], x.l[5], x.l[6], x.l[7], x.l[8], x.l[9], x.l[10], x.l[11], \
+                  x.l[12], x.l[13]
+
 // Montgomery product, finely-integrated product scanning (one 64-bit column accumulator).
-HB_MULFN Fp fp_mul(Fp a, Fp b) {
+HB_MULFN Fp fp_mul_l(HB_P14(x), HB_P14(y)) {
+  const Fp a = {{HB_L14(x)}};
+  const Fp b = {{HB_L14(y)}};
   HB_SCHED_FENCE();
   uint32_t m[NL];
   Fp r;
@@ -93,7 +105,8 @@ HB_MULFN Fp fp_mul(Fp a, Fp b) {
 }
 
 // Squaring: cross products a_i a_j (i < j) once, doubled; same reduction.
-HB_MULFN Fp fp_sqr(Fp a) {
+HB_MULFN Fp fp_sqr_l(HB_P14(x)) {
+  const Fp a = {{HB_L14(x)}};
   HB_SCHED_FENCE();
   uint32_t m[NL];
   Fp r;
@@ -127,6 +140,10 @@ HB_MULFN Fp fp_sqr(Fp a) {
   HB_SCHED_FENCE();
   return r;
 }
+
+
+HB_HD Fp fp_mul(const Fp& a, const Fp& b) { return fp_mul_l(HB_E14(a), HB_E14(b)); }
+HB_HD Fp fp_sqr(const Fp& a) { return fp_sqr_l(HB_E14(a)); }
 
 HB_HD void fp_normalize(Fp& a) {
 #pragma unroll
@@ -244,6 +261,82 @@ HB_HD bool fp_is_zero(const Fp& a) { return fp_is_zero_canon(fp_reduce_full(a));
 
 HB_HD bool fp_eq(const Fp& a, const Fp& b) { return fp_is_zero(fp_sub(a, b)); }
 
+// Variable-time inverse for public values (HB_FP_LATENCY kernels: the single-thread affine output of
+// combines and scalar multiples, whose inputs and results are public): binary extended Euclid over
+// canonical 32-bit words, ~2 x 381 shift/subtract steps instead of 381 squarings + 190 products.
+// Divergent across lanes, so kernels where every lane inverts keep the uniform Fermat form.
+template <int N>
+HB_HD bool words_is_one(const uint32_t* x) {
+  uint32_t o = x[0] ^ 1u;
+  for (int i = 1; i < N; i++) o |= x[i];
+  return o == 0;
+}
+template <int N>
+HB_HD void words_shr1(uint32_t* x, uint32_t top) {
+  for (int i = 0; i < N - 1; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+  x[N - 1] = (x[N - 1] >> 1) | (top << 31);
+}
+template <int N>
+HB_HD uint32_t words_add(uint32_t* x, const uint32_t* y) {
+  uint64_t c = 0;
+  for (int i = 0; i < N; i++) {
+    c += (uint64_t)x[i] + y[i];
+    x[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return (uint32_t)c;
+}
+template <int N>
+HB_HD uint32_t words_sub(uint32_t* x, const uint32_t* y) {  // returns the borrow
+  uint64_t br = 0;
+  for (int i = 0; i < N; i++) {
+    const uint64_t d = (uint64_t)x[i] - y[i] - br;
+    x[i] = (uint32_t)d;
+    br = (d >> 63) & 1;
+  }
+  return (uint32_t)br;
+}
+template <int N>
+HB_HD bool words_geq(const uint32_t* x, const uint32_t* y) {
+  for (int i = N - 1; i >= 0; i--)
+    if (x[i] != y[i]) return x[i] > y[i];
+  return true;
+}
+// out = a^-1 mod `mod` (odd), a canonical and nonzero
+template <int N>
+HB_HD void words_inv_vartime(const uint32_t* a, const uint32_t* mod, uint32_t* out) {
+  uint32_t u[N], v[N], x1[N], x2[N];
+  for (int i = 0; i < N; i++) {
+    u[i] = a[i];
+    v[i] = mod[i];
+    x1[i] = 0;
+    x2[i] = 0;
+  }
+  x1[0] = 1;
+  while (!words_is_one<N>(u) && !words_is_one<N>(v)) {
+    while ((u[0] & 1) == 0) {
+      words_shr1<N>(u, 0);
+      const uint32_t c = (x1[0] & 1) ? words_add<N>(x1, mod) : 0;
+      words_shr1<N>(x1, c);
+    }
+    while ((v[0] & 1) == 0) {
+      words_shr1<N>(v, 0);
+      const uint32_t c = (x2[0] & 1) ? words_add<N>(x2, mod) : 0;
+      words_shr1<N>(x2, c);
+    }
+    if (words_geq<N>(u, v)) {
+      words_sub<N>(u, v);
+      if (words_sub<N>(x1, x2)) words_add<N>(x1, mod);
+    } else {
+      words_sub<N>(v, u);
+      if (words_sub<N>(x2, x1)) words_add<N>(x2, mod);
+    }
+  }
+  const bool one_u = words_is_one<N>(u);
+  for (int i = 0; i < N; i++) out[i] = one_u ? x1[i] : x2[i];
+}
+
+#ifndef HB_FP_LATENCY
 // a^(p-2) by left-to-right binary exponentiation over a uniform (compile-time) exponent.
 HB_HD Fp fp_inv(const Fp& a) {
   Fp r = a;  // top bit of p-2 is set
@@ -254,4 +347,14 @@ HB_HD Fp fp_inv(const Fp& a) {
   return r;
 }
 
+#else
+HB_HD Fp fp_inv(const Fp& a) {
+  uint32_t w[12], p[12], r[12];
+  fp_to_words(a, w);
+  for (int i = 0; i < 12; i++) p[i] = PM2_W[i];
+  p[0] += 2;  // p - 2 + 2 (no carry: the low word of p - 2 is 0xffffaaa9)
+  words_inv_vartime<12>(w, p, r);
+  return fp_from_words(r);
+}
+#endif
 }  // namespace hb

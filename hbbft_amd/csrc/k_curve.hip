@@ -1,6 +1,8 @@
 // Curve kernels (gfx950): batched scalar multiplication, threshold_crypto interpolate() (the
 // Lagrange-at-0 MSMs behind combine_signatures and PublicKeySet::decrypt) and the SyncKeyGen
 // bivariate-commitment checks.  Host launchers at the bottom (declared in launch.hpp).
+// Variable-time Fp inverse (fp.hpp) for the single-thread affine outputs of this file's kernels.
+#define HB_FP_LATENCY 1
 #include <hip/hip_runtime.h>
 
 #include "curve.hpp"
@@ -69,67 +71,217 @@ __device__ __forceinline__ bool lagrange(const uint32_t* __restrict__ xs, int m,
   return true;
 }
 
-template <class F>
-__device__ __forceinline__ void store_jac(void* work, size_t idx, const Jac<F>& p) {
-  reinterpret_cast<Jac<F>*>(work)[idx] = p;
-}
-template <class F>
-__device__ __forceinline__ Jac<F> load_jac(const void* work, size_t idx) {
-  return reinterpret_cast<const Jac<F>*>(work)[idx];
-}
-
-__global__ void __launch_bounds__(256) k_g1_interp_terms(int ncomb, int m, const uint32_t* __restrict__ xs,
-                                                         const uint32_t* __restrict__ pts, void* __restrict__ work,
-                                                         int* __restrict__ status) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ncomb * m) return;
-  const int c = t / m, k = t % m;
-  uint32_t lam[8];
-  if (!lagrange(xs + (size_t)c * m, m, k, lam)) {
-    status[c] = hbl::HBL_DUPLICATE;
-    store_jac(work, t, jac_zero<Fp>());
-    return;
-  }
-  Fp x, y;
-  bool inf;
-  load_g1(pts + (size_t)t * G1_WORDS, x, y, inf);
-  store_jac(work, t, jac_mul_affine(x, y, inf, lam));
+// Endomorphism split of a canonical scalar k < r (r < |x|^4, x the BLS parameter):
+//   G2: k = d0 + d1|x| + d2|x|^2 + d3|x|^3 (digits < |x| < 2^64); psi = [x] on G2, so
+//       |x|^j P = (-1)^j psi^j(P) and k P = sum_j d_j (-1)^j psi^j(P).
+//   G1: k = d0 + d1 x^2 (digits < x^2 < 2^128); phi(x, y) = (beta x, y) = [-x^2] on G1, so
+//       x^2 P = (beta x, -y) and k P = d0 P + d1 (beta x, -y).
+// Digits by bit-serial long division (wave-uniform loops, no 128-bit types on the device).
+// Valid for points of the prime-order subgroups, which the ABI requires of every sample.
+HB_HD void k_to_u64(const uint32_t* k, uint64_t q[4]) {
+  for (int w = 0; w < 4; w++) q[w] = (uint64_t)k[2 * w] | ((uint64_t)k[2 * w + 1] << 32);
 }
 
-__global__ void __launch_bounds__(256) k_g2_interp_terms(int ncomb, int m, const uint32_t* __restrict__ xs,
-                                                         const uint32_t* __restrict__ pts, void* __restrict__ work,
-                                                         int* __restrict__ status) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ncomb * m) return;
-  const int c = t / m, k = t % m;
-  uint32_t lam[8];
-  if (!lagrange(xs + (size_t)c * m, m, k, lam)) {
-    status[c] = hbl::HBL_DUPLICATE;
-    store_jac(work, t, jac_zero<Fp2>());
-    return;
+// q <- q / D, returns q mod D; D = X_ABS (top bit set, so a shifted-out bit always means >= D)
+HB_HD uint64_t div_x_abs(uint64_t q[4]) {
+  uint64_t rem = 0;
+  for (int w = 3; w >= 0; w--) {
+    uint64_t qw = 0;
+    for (int b = 63; b >= 0; b--) {
+      const bool top = (rem >> 63) != 0;
+      rem = (rem << 1) | ((q[w] >> b) & 1);
+      const bool ge = top || rem >= X_ABS;
+      if (ge) rem -= X_ABS;
+      qw |= (uint64_t)ge << b;
+    }
+    q[w] = qw;
   }
+  return rem;
+}
+
+// q <- q / x^2, rem <- q mod x^2 (128-bit divisor with its top bit set)
+HB_HD void div_x2(uint64_t q[4], uint64_t rem[2]) {
+  uint64_t r0 = 0, r1 = 0;
+  for (int w = 3; w >= 0; w--) {
+    uint64_t qw = 0;
+    for (int b = 63; b >= 0; b--) {
+      const bool top = (r1 >> 63) != 0;
+      r1 = (r1 << 1) | (r0 >> 63);
+      r0 = (r0 << 1) | ((q[w] >> b) & 1);
+      const bool ge = top || r1 > X2_ABS[1] || (r1 == X2_ABS[1] && r0 >= X2_ABS[0]);
+      if (ge) {
+        const uint64_t nr0 = r0 - X2_ABS[0];
+        r1 = r1 - X2_ABS[1] - (r0 < X2_ABS[0] ? 1 : 0);
+        r0 = nr0;
+      }
+      qw |= (uint64_t)ge << b;
+    }
+    q[w] = qw;
+  }
+  rem[0] = r0;
+  rem[1] = r1;
+}
+
+HB_HD Fp2 psi_x(const Fp2& x) {  // conj(x) * (0 + c u) = (x1 c) + (x0 c) u
+  const Fp c = fp_const(PSI_C1_C1);
+  return {fp_mul(x.c1, c), fp_mul(x.c0, c)};
+}
+HB_HD Fp2 psi_y(const Fp2& y) {
+  const Fp2 c2 = {fp_const(PSI_C2_C0), fp_const(PSI_C2_C1)};
+  return f2_mul(f2_conj(y), c2);
+}
+
+// term j of the split: digit_j * base_j(P) as a Jacobian point
+__device__ __forceinline__ Jac<Fp2> endo_term(const uint32_t* w, const uint32_t* lam, int j) {
   Fp2 x, y;
   bool inf;
-  load_g2(pts + (size_t)t * G2_WORDS, x, y, inf);
-  store_jac(work, t, jac_mul_affine(x, y, inf, lam));
+  load_g2(w, x, y, inf);
+  uint64_t q[4], dg[4];
+  k_to_u64(lam, q);
+  dg[0] = div_x_abs(q);
+  dg[1] = div_x_abs(q);
+  dg[2] = div_x_abs(q);
+  dg[3] = q[0];  // the quotient after three divisions (< |x| since k < r < |x|^4)
+  const uint64_t d = j == 0 ? dg[0] : j == 1 ? dg[1] : j == 2 ? dg[2] : dg[3];
+  for (int s = 0; s < j; s++) {
+    x = psi_x(x);
+    y = psi_y(y);
+  }
+  if (j & 1) y = f2_neg(y);
+  const uint32_t kk[8] = {(uint32_t)d, (uint32_t)(d >> 32), 0, 0, 0, 0, 0, 0};
+  return jac_mul_affine(x, y, inf, kk);
+}
+__device__ __forceinline__ Jac<Fp> endo_term(const uint32_t* w, const uint32_t* lam, int j, Fp /*tag*/) {
+  Fp x, y;
+  bool inf;
+  load_g1(w, x, y, inf);
+  uint64_t q[4], rem[2];
+  k_to_u64(lam, q);
+  div_x2(q, rem);
+  uint64_t d0 = rem[0], d1 = rem[1];
+  if (j == 1) {  // x^2 P = (beta x, -y); quotient < x^2 < 2^128
+    d0 = q[0];
+    d1 = q[1];
+    x = fp_mul(x, fp_const(BETA_M));
+    y = fp_neg(y);
+  }
+  const uint32_t kk[8] = {(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32), 0, 0, 0, 0};
+  return jac_mul_affine(x, y, inf, kk);
 }
 
-__global__ void __launch_bounds__(64) k_g1_interp_sum(int ncomb, int m, const void* __restrict__ work,
-                                                      uint32_t* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncomb) return;
-  Jac<Fp> acc = load_jac<Fp>(work, (size_t)c * m);
-  for (int k = 1; k < m; k++) acc = jac_add(acc, load_jac<Fp>(work, (size_t)c * m + k));
-  g1_jac_to_words(acc, out + (size_t)c * G1_WORDS);
+template <class F>
+struct EndoSplit;
+template <>
+struct EndoSplit<Fp2> {
+  static constexpr int N = 4, WORDS = G2_WORDS;
+  __device__ static Jac<Fp2> term(const uint32_t* w, const uint32_t* lam, int j) { return endo_term(w, lam, j); }
+  __device__ static void store(const Jac<Fp2>& p, uint32_t* out) { g2_jac_to_words(p, out); }
+};
+template <>
+struct EndoSplit<Fp> {
+  static constexpr int N = 2, WORDS = G1_WORDS;
+  __device__ static Jac<Fp> term(const uint32_t* w, const uint32_t* lam, int j) { return endo_term(w, lam, j, Fp{}); }
+  __device__ static void store(const Jac<Fp>& p, uint32_t* out) { g1_jac_to_words(p, out); }
+};
+
+// numerator / denominator of lambda_k(0) (Montgomery); false when some x_j == x_k (j != k)
+__device__ __forceinline__ bool lagrange_parts(const uint32_t* __restrict__ xs, int m, int k, Fr& num, Fr& den) {
+  num = fr_raw(FR_ONE_M);
+  den = fr_raw(FR_ONE_M);
+  const Fr xk = fr_from_u32(xs[k]);
+  for (int j = 0; j < m; j++) {
+    if (j == k) continue;
+    const Fr xj = fr_from_u32(xs[j]);
+    num = fr_mul(num, xj);
+    den = fr_mul(den, fr_sub(xj, xk));
+  }
+  return !fr_is_zero(den);
 }
 
-__global__ void __launch_bounds__(64) k_g2_interp_sum(int ncomb, int m, const void* __restrict__ work,
-                                                      uint32_t* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncomb) return;
-  Jac<Fp2> acc = load_jac<Fp2>(work, (size_t)c * m);
-  for (int k = 1; k < m; k++) acc = jac_add(acc, load_jac<Fp2>(work, (size_t)c * m + k));
-  g2_jac_to_words(acc, out + (size_t)c * G2_WORDS);
+// variable-time Fr inverse (one thread, public denominators)
+__device__ __forceinline__ Fr fr_inv_vartime(const Fr& a) {
+  const Fr c = fr_to_canon(a);
+  uint32_t r[FRL];
+  words_inv_vartime<FRL>(c.l, FR_W, r);
+  Fr t;
+  for (int j = 0; j < FRL; j++) t.l[j] = r[j];
+  return fr_mul(t, fr_raw(FR_R2));  // canonical -> Montgomery
+}
+
+// One workgroup per combine.
+//  Phase 1: thread k < m forms num_k and den_k of lambda_k(0) = prod x_j / prod (x_j - x_k); thread 0
+//           inverts all den_k with one (variable-time) inversion (Montgomery's batch trick: 3m
+//           products) and stages the canonical lambda_k in LDS.
+//  Phase 2: thread t < m*N computes term (k, j) = (t / N, t % N): lambda_k(0) * P_k restricted to
+//           endomorphism digit j (64-bit scalar on G2, 128-bit on G1) -- a serial doubling chain of
+//           64 (G2) / 128 (G1) steps instead of 255.
+//  Phase 3: tree sum of the terms in LDS; thread 0 writes the affine result.
+// Combines with m > LAM_LDS_MAX samples compute lambda per term instead (uniform Fermat inverse).
+constexpr int LAM_LDS_MAX = 256;
+
+template <class F>
+__global__ void __launch_bounds__(256) k_interp_endo(int ncomb, int m, const uint32_t* __restrict__ xs,
+                                                     const uint32_t* __restrict__ pts, uint32_t* __restrict__ out,
+                                                     int* __restrict__ status) {
+  extern __shared__ unsigned char smem_raw[];
+  __shared__ int s_dup;
+  Jac<F>* sm = reinterpret_cast<Jac<F>*>(smem_raw);
+  Fr* snum = reinterpret_cast<Fr*>(smem_raw + blockDim.x * sizeof(Jac<F>));
+  Fr* sden = snum + m;
+  Fr* slam = sden + m;  // prefix products, then the canonical lambda_k
+  using S = EndoSplit<F>;
+  const int c = blockIdx.x;
+  if (c >= ncomb) return;  // uniform per workgroup
+  const uint32_t* cx = xs + (size_t)c * m;
+  const bool staged = m <= LAM_LDS_MAX;
+  if (staged) {
+    if (threadIdx.x == 0) s_dup = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < m; k += blockDim.x) {
+      Fr num, den;
+      if (!lagrange_parts(cx, m, k, num, den)) s_dup = 1;
+      snum[k] = num;
+      sden[k] = den;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (s_dup) {
+        status[c] = hbl::HBL_DUPLICATE;  // the combine's output is void; its terms are O
+        for (int k = 0; k < m; k++)
+          for (int w = 0; w < FRL; w++) slam[k].l[w] = 0;
+      } else {
+        slam[0] = sden[0];
+        for (int k = 1; k < m; k++) slam[k] = fr_mul(slam[k - 1], sden[k]);
+        Fr inv = fr_inv_vartime(slam[m - 1]);
+        for (int k = m - 1; k > 0; k--) {
+          const Fr ik = fr_mul(inv, slam[k - 1]);
+          inv = fr_mul(inv, sden[k]);
+          slam[k] = fr_to_canon(fr_mul(snum[k], ik));
+        }
+        slam[0] = fr_to_canon(fr_mul(snum[0], inv));
+      }
+    }
+    __syncthreads();
+  }
+  Jac<F> acc = jac_zero<F>();
+  for (int t = threadIdx.x; t < m * S::N; t += blockDim.x) {
+    const int k = t / S::N, j = t % S::N;
+    uint32_t lam[8];
+    if (staged) {
+      for (int w = 0; w < 8; w++) lam[w] = slam[k].l[w];
+    } else if (!lagrange(cx, m, k, lam)) {
+      status[c] = hbl::HBL_DUPLICATE;
+      continue;
+    }
+    acc = jac_add(acc, S::term(pts + ((size_t)c * m + k) * S::WORDS, lam, j));
+  }
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sm[threadIdx.x] = jac_add(sm[threadIdx.x], sm[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) S::store(sm[0], out + (size_t)c * S::WORDS);
 }
 
 // ------------------------------------------------------------------ SyncKeyGen
@@ -198,27 +350,22 @@ hipError_t g2_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars
   return hipGetLastError();
 }
 
-size_t combine_work_bytes(int ncomb, int m, int g2) {
-  return (size_t)ncomb * m * (g2 ? sizeof(hb::Jac<hb::Fp2>) : sizeof(hb::Jac<hb::Fp>));
-}
-
-hipError_t combine_g1(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* work, void* out,
-                      int* status) {
+template <class F>
+static hipError_t combine(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out,
+                          int* status) {
   if (ncomb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hb::k_g1_interp_terms, grid_for(ncomb * m), dim3(256), 0, s, ncomb, m, xs, (const uint32_t*)pts,
-                     work, status);
-  hipLaunchKernelGGL(hb::k_g1_interp_sum, grid_for(ncomb, 64), dim3(64), 0, s, ncomb, m, (const void*)work,
-                     (uint32_t*)out);
+  int b = 64;  // power of two >= m * N (tree reduction), 64..256
+  while (b < 256 && b < m * hb::EndoSplit<F>::N) b *= 2;
+  const size_t lds = b * sizeof(hb::Jac<F>) + (m <= hb::LAM_LDS_MAX ? (size_t)m * 3 * sizeof(hb::Fr) : 0);
+  hipLaunchKernelGGL(hb::k_interp_endo<F>, dim3((unsigned)ncomb), dim3(b), lds, s, ncomb, m, xs,
+                     (const uint32_t*)pts, (uint32_t*)out, status);
   return hipGetLastError();
 }
-hipError_t combine_g2(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* work, void* out,
-                      int* status) {
-  if (ncomb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hb::k_g2_interp_terms, grid_for(ncomb * m), dim3(256), 0, s, ncomb, m, xs, (const uint32_t*)pts,
-                     work, status);
-  hipLaunchKernelGGL(hb::k_g2_interp_sum, grid_for(ncomb, 64), dim3(64), 0, s, ncomb, m, (const void*)work,
-                     (uint32_t*)out);
-  return hipGetLastError();
+hipError_t combine_g1(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out, int* status) {
+  return combine<hb::Fp>(s, ncomb, m, xs, pts, out, status);
+}
+hipError_t combine_g2(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out, int* status) {
+  return combine<hb::Fp2>(s, ncomb, m, xs, pts, out, status);
 }
 
 hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const uint32_t* part_idx, const uint32_t* xs,

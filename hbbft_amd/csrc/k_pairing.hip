@@ -1,4 +1,4 @@
-// Pairing-equality kernels (kernels.hpp) and their host launchers.
+// One-thread-per-check pairing kernels (HBH_IMPL_THREAD, kernels.hpp) and their host launchers.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -7,15 +7,6 @@
 namespace hbl {
 
 static inline dim3 grid_for(int n) { return dim3((unsigned)((n + 255) / 256)); }
-
-hipError_t g2_prepare(hipStream_t s, int n0, const void* pts0, void* coef0, uint8_t* inf0, int n1, const void* pts1,
-                      void* coef1, uint8_t* inf1) {
-  if (n0 + n1 <= 0) return hipSuccess;
-  hb::PrepSet a{n0, (const uint32_t*)pts0, pad64(n0), (uint4*)coef0, inf0};
-  hb::PrepSet b{n1, (const uint32_t*)pts1, pad64(n1), (uint4*)coef1, inf1};
-  hipLaunchKernelGGL(hb::k_g2_prepare, grid_for(n0 + n1), dim3(256), 0, s, a, b);
-  return hipGetLastError();
-}
 
 hipError_t pairing_eq(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
                       const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,

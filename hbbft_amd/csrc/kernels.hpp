@@ -1,84 +1,8 @@
 // Batch kernels of the pairing-equality path (gfx950).
 #pragma once
-#include "pairing.hpp"
-#include "points.hpp"
+#include "lines.hpp"
 
 namespace hb {
-
-constexpr int LINE_Q4 = LINE_WORDS / 4;  // 21 x 16-byte chunks per line
-
-// Line tables: uint4 coef[(step * LINE_Q4 + q) * stride + point]  -- lanes that walk consecutive
-// points read consecutive 16-byte chunks (coalesced); lanes sharing a point (H per document) read
-// one broadcast address.
-__device__ __forceinline__ void store_line(uint4* __restrict__ coef, int stride, int step, int pt, const Line& l) {
-  uint32_t w[LINE_WORDS];
-#pragma unroll
-  for (int j = 0; j < NL; j++) {
-    w[0 * NL + j] = l.c0.c0.l[j];
-    w[1 * NL + j] = l.c0.c1.l[j];
-    w[2 * NL + j] = l.c1.c0.l[j];
-    w[3 * NL + j] = l.c1.c1.l[j];
-    w[4 * NL + j] = l.c4.c0.l[j];
-    w[5 * NL + j] = l.c4.c1.l[j];
-  }
-#pragma unroll
-  for (int q = 0; q < LINE_Q4; q++)
-    coef[((size_t)step * LINE_Q4 + q) * stride + pt] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-}
-
-__device__ __forceinline__ Line load_line(const uint4* __restrict__ coef, int stride, int step, int pt) {
-  uint32_t w[LINE_WORDS];
-#pragma unroll
-  for (int q = 0; q < LINE_Q4; q++) {
-    uint4 v = coef[((size_t)step * LINE_Q4 + q) * stride + pt];
-    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-  }
-  Line l;
-#pragma unroll
-  for (int j = 0; j < NL; j++) {
-    l.c0.c0.l[j] = w[0 * NL + j];
-    l.c0.c1.l[j] = w[1 * NL + j];
-    l.c1.c0.l[j] = w[2 * NL + j];
-    l.c1.c1.l[j] = w[3 * NL + j];
-    l.c4.c0.l[j] = w[4 * NL + j];
-    l.c4.c1.l[j] = w[5 * NL + j];
-  }
-  return l;
-}
-
-// Walk T over the Miller loop of Q and store its 68 lines.  Two independent point sets share one
-// launch (the per-document H table and the per-share G2 points): the small set's latency-bound
-// walk then overlaps the large one instead of adding a serial launch.
-struct PrepSet {
-  int n;
-  const uint32_t* pts;
-  int stride;
-  uint4* coef;
-  uint8_t* inf;
-};
-__global__ void __launch_bounds__(256) k_g2_prepare(PrepSet s0, PrepSet s1) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool first = i < s0.n;
-  if (!first) i -= s0.n;
-  if (!first && i >= s1.n) return;
-  const uint32_t* pts = first ? s0.pts : s1.pts;
-  const int stride = first ? s0.stride : s1.stride;
-  uint4* coef = first ? s0.coef : s1.coef;
-  uint8_t* inf = first ? s0.inf : s1.inf;
-  G2Aff q = g2_from_words(pts + (size_t)i * G2_WORDS);
-  inf[i] = q.inf ? 1 : 0;
-  if (q.inf) { q.x = f2_one(); q.y = f2_one(); }  // dummy walk; the pair is masked out
-  G2Jac T{q.x, q.y, f2_one()};
-  int step = 0;
-  for (int b = 62; b >= 0; b--) {
-    Line l = dbl_step(T);
-    store_line(coef, stride, step++, i, l);
-    if ((X_ABS >> b) & 1) {
-      l = add_step(T, q.x, q.y);
-      store_line(coef, stride, step++, i, l);
-    }
-  }
-}
 
 __device__ __forceinline__ Fp12 mul_line_masked(const Fp12& f, const Line& l, const Fp& xP, const Fp& yP, bool active) {
   Fp2 c0 = f2_sel(active, l.c0, f2_one());

@@ -51,13 +51,10 @@ hipError_t g1_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars
 hipError_t g2_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars, void* out);
 // Lagrange interpolation at 0 (threshold_crypto interpolate) of `ncomb` combines of m = t+1
 // samples each: x[c*m + k] = idx + 1 (Fr, small integers), pts[c*m + k] the samples.
-// status[c] (zeroed by the caller) becomes HBL_DUPLICATE when two x coincide.  work: scratch of
-// combine_work_bytes().  out: ncomb affine points (ABI words).
-hipError_t combine_g1(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* work, void* out,
-                      int* status);
-hipError_t combine_g2(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* work, void* out,
-                      int* status);
-size_t combine_work_bytes(int ncomb, int m, int g2);
+// status[c] (zeroed by the caller) becomes HBL_DUPLICATE when two x coincide.  out: ncomb affine
+// points (ABI words).  One workgroup per combine (endomorphism-split terms + LDS tree sum).
+hipError_t combine_g1(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out, int* status);
+hipError_t combine_g2(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out, int* status);
 // BivarCommitment::row(x) (t+1 outputs) for nrow (part, x) pairs; commit = (t+1)(t+2)/2 G1 points
 // per part.  out[r*(t+1) + i].
 hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const uint32_t* part_idx, const uint32_t* xs,

@@ -133,13 +133,18 @@ int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, cons
                         uint8_t* verdicts);
 
 /* ---------------------------------------------------------------- implementation selection
- * Two pairing implementations with identical verdicts: HBH_IMPL_THREAD (default: one thread per
- * check, 37.6 ms per 65,536 checks on MI355X) and HBH_IMPL_LANE_COOP (six lanes per check, one Fp2
- * coefficient of the Fp12 accumulator per lane; 47 ms today).  Selectable for A/B measurement and
- * cross-checking. */
+ * Three pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks
+ * them): HBH_IMPL_THREAD (one thread per check, 14x28-bit unsigned limbs, k_pairing.hip),
+ * HBH_IMPL_LANE_COOP (six lanes per check, one Fp2 coefficient of the Fp12 accumulator per lane;
+ * lowest latency for small batches) and HBH_IMPL_THREAD_SIGNED (one thread per check on signed
+ * limbs, stage kernels k_ts_*.hip; highest throughput).  HBH_IMPL_AUTO (the default) picks
+ * LANE_COOP below HBH_AUTO_LANE_COOP_MAX checks per call and THREAD_SIGNED from there on
+ * (7 ms vs 27 ms for one check, 47 ms vs 26.5 ms for 65,536). */
 #define HBH_IMPL_THREAD 0
 #define HBH_IMPL_LANE_COOP 1
-#define HBH_IMPL_THREAD_SIGNED 2 /* one thread per check on signed limbs, stage kernels (k_ts_*.hip) */
+#define HBH_IMPL_THREAD_SIGNED 2
+#define HBH_IMPL_AUTO 3
+#define HBH_AUTO_LANE_COOP_MAX 16384
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 
 /* ---------------------------------------------------------------- profiling

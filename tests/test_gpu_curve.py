@@ -89,6 +89,25 @@ def test_interpolate_edge_cases(engine):
     assert st == [0] and out == [bytes(96)]
 
 
+@pytest.mark.parametrize("t", [1, 5, 21, 70])
+def test_interpolate_random_samples_match_oracle(engine, t):
+    """Arbitrary subgroup points (not shares of one polynomial), ragged index sets, an infinity
+    sample, and t = 70 (284 G2 / 142 G1 endomorphism terms: more terms than threads per combine)
+    -- byte-identical to the C restatement of threshold_crypto interpolate()."""
+    rng = random.Random(100 + t)
+    m = t + 1
+    idx = [sorted(rng.sample(range(200), m)) for _ in range(3)]
+    p2 = [[cbls.g2_mul(G2, rng.randrange(1, C.R)) for _ in range(m)] for _ in range(3)]
+    p1 = [[cbls.g1_mul(G1, rng.randrange(1, C.R)) for _ in range(m)] for _ in range(3)]
+    p2[1][0], p1[2][m - 1] = bytes(192), bytes(96)
+    out, st = engine.interpolate_g2(t, idx, p2)
+    assert st == [0, 0, 0]
+    assert out == [cbls.combine_g2(t, i, p)[1] for i, p in zip(idx, p2)]
+    out, st = engine.interpolate_g1(t, idx, p1)
+    assert st == [0, 0, 0]
+    assert out == [cbls.combine_g1(t, i, p)[1] for i, p in zip(idx, p1)]
+
+
 def test_threshold_decrypt_golden(engine):
     d = load("threshold_decrypt_n10_t3.json")
     t = d["t"]

@@ -13,13 +13,13 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[1, 2, 0], ids=["lane_coop", "thread_signed", "thread"])
+@pytest.fixture(params=[1, 2, 0, 3], ids=["lane_coop", "thread_signed", "thread", "auto"])
 def eng(engine, request):
-    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_THREAD) must
-    give identical results."""
+    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_THREAD, and
+    the default HBH_IMPL_AUTO) must give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine
-    engine.set_pairing_impl(0)
+    engine.set_pairing_impl(3)
 
 
 def load(name):
@@ -124,6 +124,7 @@ def test_lane_coop_matches_thread_random_batch(engine):
     v2 = engine.verify_sig_shares(P, S, hs, D)
     engine.set_pairing_impl(0)
     v0 = engine.verify_sig_shares(P, S, hs, D)
+    engine.set_pairing_impl(3)
     assert v1 == v0
     assert v2 == v0
     for i, w in want:
