@@ -154,8 +154,7 @@ def combine_latency(eng, w, reps=7):
     times = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        out, st = eng.interpolate_g2(T, [idx], [pts])
-        v = eng.verify_sig_shares([w.master_pk], [out[0]], [w.hashes[0]], [0])
+        out, st, v = eng.combine_verify_g2(T, [idx], [pts], w.master_pk, [w.hashes[0]])
         times.append((time.perf_counter() - t0) * 1e3)
         assert st == [0] and v == b"\x01", "combined signature does not verify"
     ndocs = len(w.hashes)

@@ -32,6 +32,7 @@ SIGNATURES = [
     ("hbh_dbg_pairing", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_interpolate_g2", _I, [_P, _SZ, _I, _P, _P, _P, _P]),
     ("hbh_interpolate_g1", _I, [_P, _SZ, _I, _P, _P, _P, _P]),
+    ("hbh_combine_verify_g2", _I, [_P, _SZ, _I, _P, _P, _P, _P, _P, _P, _P]),
     ("hbh_g1_mul", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_g2_mul", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_bivar_row", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),

@@ -458,6 +458,61 @@ int hbh_interpolate_g1(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, 
   return run_interp(e, ncomb, t, idx, pts, out, status, false);
 }
 
+// ThresholdSign::combine_and_verify_sig (src/threshold_sign.rs:249-270) as one device pass: the
+// interpolated signature stays in HBM and feeds the master check e(pk, H_c) == e(g1, sig_c) on the
+// same stream -- no host round trip between combine and verify.
+int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const uint8_t* shares,
+                          const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out, int* status,
+                          uint8_t* verdicts) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (ncomb == 0) return HBH_OK;
+  if (!idx || !shares || !master_pk || !hashes || !out || !status || !verdicts) return fail(HBH_ERR_ARG, "null pointer");
+  const size_t m = (size_t)t + 1;
+  if (ncomb * m > (size_t)1 << 26) return fail(HBH_ERR_ARG, "batch too large");
+  std::vector<uint32_t> xs(ncomb * m);
+  for (size_t k = 0; k < ncomb * m; k++) {
+    if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
+    xs[k] = idx[k] + 1;
+  }
+  // P1 = master pk (repeated), P2 = g1 (repeated): one staging buffer, pk records then g1 records
+  std::vector<uint8_t> p12(2 * ncomb * HBH_G1_BYTES);
+  const std::vector<uint8_t>& g1 = g1_generator_bytes();
+  for (size_t c = 0; c < ncomb; c++) {
+    std::memcpy(p12.data() + c * HBH_G1_BYTES, master_pk, HBH_G1_BYTES);
+    std::memcpy(p12.data() + (ncomb + c) * HBH_G1_BYTES, g1.data(), HBH_G1_BYTES);
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
+  HBH_CHECK(e->in_b.ensure(ncomb * m * HBH_G2_BYTES));
+  HBH_CHECK(e->in_q1.ensure(ncomb * HBH_G2_BYTES));
+  HBH_CHECK(e->in_p1.ensure(p12.size()));
+  HBH_CHECK(e->out_x.ensure(ncomb * HBH_G2_BYTES));
+  HBH_CHECK(e->status.ensure(ncomb * sizeof(int)));
+  HBH_CHECK(e->out_v.ensure(ncomb));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xs.data(), ncomb * m * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, shares, ncomb * m * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_q1.p, hashes, ncomb * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p12.data(), p12.size(), hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
+                            (int*)e->status.p));
+  e->timer.end(s, tm);
+  const uint8_t* d_p = (const uint8_t*)e->in_p1.p;
+  rc = run_pairing_eq_dev(e, s, ncomb, d_p, e->in_q1.p, ncomb, nullptr, d_p + ncomb * HBH_G1_BYTES, e->out_x.p, ncomb,
+                          nullptr, (uint8_t*)e->out_v.p);
+  if (rc) return rc;
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * HBH_G2_BYTES, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, ncomb, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
 int hbh_bivar_row(hbh_engine* e, size_t nrow, int t, size_t nparts, const uint8_t* commits, const uint32_t* part_idx,
                   const uint32_t* xs, uint8_t* out) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");

@@ -137,6 +137,29 @@ class Engine:
         """PublicKeySet::combine_signatures batch (src/threshold_sign.rs:249-259): (points, status)."""
         return self._interp(self._l.hbh_interpolate_g2, G2_BYTES, t, idx, pts)
 
+    def combine_verify_g2(self, t, idx, pts, master_pk, hashes):
+        """ThresholdSign::combine_and_verify_sig batch (src/threshold_sign.rs:249-270): one device
+        pass of combine_signatures + PublicKey::verify_g2 per document.  Returns
+        (signatures, statuses, verdicts); hashes[c] is H of document c."""
+        ncomb = len(idx)
+        if any(len(row) != t + 1 for row in idx):
+            raise ValueError("each combine needs exactly t+1 samples")
+        pb = _join([p for row in pts for p in row] if ncomb and isinstance(pts[0], (list, tuple)) else pts, G2_BYTES)
+        hb = _join(hashes, G2_BYTES)
+        if len(pb) != ncomb * (t + 1) * G2_BYTES or len(hb) != ncomb * G2_BYTES or len(bytes(master_pk)) != G1_BYTES:
+            raise ValueError("point count mismatch")
+        ia, pia = _u32([int(i) for row in idx for i in row], ncomb * (t + 1))
+        out = (ctypes.c_uint8 * max(ncomb * G2_BYTES, 1))()
+        st = (ctypes.c_int * max(ncomb, 1))()
+        v = (ctypes.c_uint8 * max(ncomb, 1))()
+        keep = [buf(x) for x in (pb, bytes(master_pk), hb)]
+        check(self._l.hbh_combine_verify_g2(self._h, ncomb, t, pia, keep[0][1], keep[1][1], keep[2][1],
+                                            ctypes.cast(out, ctypes.c_void_p), ctypes.cast(st, ctypes.c_void_p),
+                                            ctypes.cast(v, ctypes.c_void_p)))
+        raw = bytes(out)
+        return ([raw[c * G2_BYTES:(c + 1) * G2_BYTES] for c in range(ncomb)], list(st)[:ncomb],
+                bytes(v)[:ncomb])
+
     def interpolate_g1(self, t, idx, pts):
         """G1 interpolation of PublicKeySet::decrypt (src/threshold_decrypt.rs:242-250)."""
         return self._interp(self._l.hbh_interpolate_g1, G1_BYTES, t, idx, pts)

@@ -234,10 +234,11 @@ class ThresholdSign:
     def combine_and_verify_sig(self):  # :249-270
         t = self.netinfo.num_faulty()
         items = [self.received_shares[k] for k in sorted(self.received_shares)][: t + 1]
-        out, st = self.verifier.eng.interpolate_g2(t, [[i for i, _ in items]], [[s for _, s in items]])
+        out, st, v = self.verifier.eng.combine_verify_g2(t, [[i for i, _ in items]], [[s for _, s in items]],
+                                                         self.netinfo.master_pk, [self.doc_hash])
         if st[0] != 0:
             raise ProtocolError("CombineAndVerifySigCrypto", "DuplicateEntry")
-        if not self.verifier.eng.verify_sig_shares([self.netinfo.master_pk], [out[0]], [self.doc_hash], [0])[0]:
+        if not v[0]:
             raise ProtocolError("VerificationFailed")
         return out[0]
 

@@ -110,6 +110,16 @@ int hbh_interpolate_g2(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx
 int hbh_interpolate_g1(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out,
                        int* status);
 
+/* ThresholdSign::combine_and_verify_sig (src/threshold_sign.rs:249-270) for `ncomb` documents in
+ * one device pass: out[c] = combine_signatures(first t+1 shares) as hbh_interpolate_g2, then
+ * verdict[c] = PublicKey::verify_g2(out[c], hashes[c]) = (e(master_pk, H_c) == e(g1, out[c]))
+ * (:260-266) without a host round trip in between.  status[c] as hbh_interpolate_g2; verdict[c]
+ * = 0 is the reference's Error::VerificationFailed; verdicts of a combine whose status is not
+ * HBH_OK are meaningless (the reference returns the combine error first). */
+int hbh_combine_verify_g2(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx, const uint8_t* shares,
+                          const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out, int* status,
+                          uint8_t* verdicts);
+
 /* ---------------------------------------------------------------- scalar multiplication
  * out[i] = k_i * P_i, k_i a 32-byte little-endian integer (any value < 2^256).  Public-data helper
  * for commitments (Poly::commitment = g1 * c_i, src/sync_key_gen.rs:508), public-key-share

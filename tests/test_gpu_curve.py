@@ -72,6 +72,42 @@ def test_interpolate_g2_n64_t21_matches_oracle(engine):
     assert cbls.combine_g2(t, idx[1], pts[1]) == (0, want)
 
 
+def test_combine_verify_g2_matches_two_step(engine):
+    """hbh_combine_verify_g2 (combine_and_verify_sig, src/threshold_sign.rs:249-270): same signature
+    as interpolate_g2, master-key verdict as the C oracle's verify_g2; a wrong document hash gives
+    VerificationFailed (verdict 0), a duplicate index DuplicateEntry."""
+    rng = random.Random(22)
+    t = 21
+    msk = rng.randrange(1, C.R)
+    coeffs = [msk] + [rng.randrange(1, C.R) for _ in range(t)]
+    mpk = cbls.g1_mul(G1, msk)
+    hs = [cbls.g2_mul(G2, rng.randrange(1, C.R)) for _ in range(3)]
+    idx, pts = [], []
+    for h in hs:
+        sub = sorted(rng.sample(range(64), t + 1))
+        idx.append(sub)
+        pts.append([cbls.g2_mul(h, tc.poly_eval(coeffs, i + 1)) for i in sub])
+    hashes = [hs[0], hs[1], hs[0]]  # third combine checked against the wrong document
+    idx.append([idx[0][0]] + idx[0][:t])  # duplicate index
+    pts.append(pts[0])
+    hashes.append(hs[0])
+    out, st, v = engine.combine_verify_g2(t, idx, pts, mpk, hashes)
+    assert st == [0, 0, 0, 5]
+    want = [cbls.g2_mul(h, msk) for h in hs]
+    assert out[:3] == want
+    assert list(v[:3]) == [1, 1, 0]
+    assert [cbls.verify_g2(mpk, s, h) for s, h in zip(out[:3], hashes[:3])] == [True, True, False]
+    golden = load("threshold_sign_n10_t3.json")
+    doc = golden["docs"][0]
+    by_idx = {s["idx"]: s for s in doc["shares"]}
+    gi = doc["combine_indices"]
+    out, st, v = engine.combine_verify_g2(golden["t"], [gi], [[g2a(bytes.fromhex(by_idx[i]["sig"])) for i in gi]],
+                                          g1a(C.g1_uncompressed(C.g1_decompress(bytes.fromhex(golden["master_pk"])))),
+                                          [g2a(bytes.fromhex(doc["hash"]))])
+    assert st == [0] and v == b"\x01"
+    assert out[0] == g2a(bytes.fromhex(doc["combined_uncompressed"]))
+
+
 def test_interpolate_edge_cases(engine):
     rng = random.Random(3)
     # t = 0 returns the sample itself
