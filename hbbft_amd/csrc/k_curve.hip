@@ -132,7 +132,19 @@ HB_HD Fp2 psi_y(const Fp2& y) {
 }
 
 // term j of the split: digit_j * base_j(P) as a Jacobian point
-__device__ __forceinline__ Jac<Fp2> endo_term(const uint32_t* w, const uint32_t* lam, int j) {
+// Keep 32-bit words [chunk * words / nchunk, (chunk + 1) * words / nchunk) of a digit of `words` words,
+// shifted down to bit 0 (k_interp_endo's chunked chains: digit = sum_s chunk_s * 2^(s * bits)).
+__device__ __forceinline__ void take_chunk(uint32_t kk[8], int words, int chunk, int nchunk) {
+  const int wpc = words / nchunk, lo = chunk * wpc;
+  const uint32_t t0 = kk[0], t1 = kk[1], t2 = kk[2], t3 = kk[3];
+  for (int i = 0; i < 4; i++) {
+    const int src = lo + i;
+    const uint32_t v = src == 0 ? t0 : src == 1 ? t1 : src == 2 ? t2 : t3;
+    kk[i] = (i < wpc && src < 4) ? v : 0u;
+  }
+}
+
+__device__ __forceinline__ Jac<Fp2> endo_term(const uint32_t* w, const uint32_t* lam, int j, int chunk, int nchunk) {
   Fp2 x, y;
   bool inf;
   load_g2(w, x, y, inf);
@@ -148,10 +160,12 @@ __device__ __forceinline__ Jac<Fp2> endo_term(const uint32_t* w, const uint32_t*
     y = psi_y(y);
   }
   if (j & 1) y = f2_neg(y);
-  const uint32_t kk[8] = {(uint32_t)d, (uint32_t)(d >> 32), 0, 0, 0, 0, 0, 0};
+  uint32_t kk[8] = {(uint32_t)d, (uint32_t)(d >> 32), 0, 0, 0, 0, 0, 0};
+  take_chunk(kk, 2, chunk, nchunk);
   return jac_mul_affine(x, y, inf, kk);
 }
-__device__ __forceinline__ Jac<Fp> endo_term(const uint32_t* w, const uint32_t* lam, int j, Fp /*tag*/) {
+__device__ __forceinline__ Jac<Fp> endo_term(const uint32_t* w, const uint32_t* lam, int j, int chunk, int nchunk,
+                                             Fp /*tag*/) {
   Fp x, y;
   bool inf;
   load_g1(w, x, y, inf);
@@ -165,7 +179,8 @@ __device__ __forceinline__ Jac<Fp> endo_term(const uint32_t* w, const uint32_t* 
     x = fp_mul(x, fp_const(BETA_M));
     y = fp_neg(y);
   }
-  const uint32_t kk[8] = {(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32), 0, 0, 0, 0};
+  uint32_t kk[8] = {(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32), 0, 0, 0, 0};
+  take_chunk(kk, 4, chunk, nchunk);
   return jac_mul_affine(x, y, inf, kk);
 }
 
@@ -173,14 +188,18 @@ template <class F>
 struct EndoSplit;
 template <>
 struct EndoSplit<Fp2> {
-  static constexpr int N = 4, WORDS = G2_WORDS;
-  __device__ static Jac<Fp2> term(const uint32_t* w, const uint32_t* lam, int j) { return endo_term(w, lam, j); }
+  static constexpr int N = 4, WORDS = G2_WORDS, DIGIT_WORDS = 2;  // 64-bit digits
+  __device__ static Jac<Fp2> term(const uint32_t* w, const uint32_t* lam, int j, int c, int nc) {
+    return endo_term(w, lam, j, c, nc);
+  }
   __device__ static void store(const Jac<Fp2>& p, uint32_t* out) { g2_jac_to_words(p, out); }
 };
 template <>
 struct EndoSplit<Fp> {
-  static constexpr int N = 2, WORDS = G1_WORDS;
-  __device__ static Jac<Fp> term(const uint32_t* w, const uint32_t* lam, int j) { return endo_term(w, lam, j, Fp{}); }
+  static constexpr int N = 2, WORDS = G1_WORDS, DIGIT_WORDS = 4;  // 128-bit digits
+  __device__ static Jac<Fp> term(const uint32_t* w, const uint32_t* lam, int j, int c, int nc) {
+    return endo_term(w, lam, j, c, nc, Fp{});
+  }
   __device__ static void store(const Jac<Fp>& p, uint32_t* out) { g1_jac_to_words(p, out); }
 };
 
@@ -212,17 +231,21 @@ __device__ __forceinline__ Fr fr_inv_vartime(const Fr& a) {
 //  Phase 1: thread k < m forms num_k and den_k of lambda_k(0) = prod x_j / prod (x_j - x_k); thread 0
 //           inverts all den_k with one (variable-time) inversion (Montgomery's batch trick: 3m
 //           products) and stages the canonical lambda_k in LDS.
-//  Phase 2: thread t < m*N computes term (k, j) = (t / N, t % N): lambda_k(0) * P_k restricted to
-//           endomorphism digit j (64-bit scalar on G2, 128-bit on G1) -- a serial doubling chain of
-//           64 (G2) / 128 (G1) steps instead of 255.
-//  Phase 3: tree sum of the terms in LDS; thread 0 writes the affine result.
+//  Phase 2: each digit (64-bit on G2, 128-bit on G1) is cut into nchunk 32-bit-aligned chunks.
+//           Thread (chunk s, slot t < m*N) computes term (k, j) = (t / N, t % N): chunk s of
+//           endomorphism digit j of lambda_k(0), times base_j(P_k) -- a serial double-and-add chain of
+//           64 / nchunk (G2) or 128 / nchunk (G1) steps instead of 255.
+//  Phase 3: tree sum of each chunk's terms in LDS; thread 0 joins the chunk sums by Horner
+//           (R = sum_s 2^(s*bits) S_s: the doublings run once, on the sum, without per-step adds)
+//           and writes the affine result.  For m = 22: G2 chain 32 (dbl+add) + 32 dbl instead of
+//           64 (dbl+add); G1 32 (dbl+add) + 96 dbl instead of 128 (dbl+add).
 // Combines with m > LAM_LDS_MAX samples compute lambda per term instead (uniform Fermat inverse).
 constexpr int LAM_LDS_MAX = 256;
 
 template <class F>
 __global__ void __launch_bounds__(256) k_interp_endo(int ncomb, int m, const uint32_t* __restrict__ xs,
                                                      const uint32_t* __restrict__ pts, uint32_t* __restrict__ out,
-                                                     int* __restrict__ status) {
+                                                     int* __restrict__ status, int nchunk) {
   extern __shared__ unsigned char smem_raw[];
   __shared__ int s_dup;
   Jac<F>* sm = reinterpret_cast<Jac<F>*>(smem_raw);
@@ -263,8 +286,11 @@ __global__ void __launch_bounds__(256) k_interp_endo(int ncomb, int m, const uin
     }
     __syncthreads();
   }
+  // thread -> (chunk, slot): group `chunk` of G = blockDim / nchunk threads sums chunk `chunk` of
+  // every term's digit, so each chain is (digit bits / nchunk) steps instead of digit bits.
+  const int G = blockDim.x / nchunk, chunk = threadIdx.x / G, g = threadIdx.x % G;
   Jac<F> acc = jac_zero<F>();
-  for (int t = threadIdx.x; t < m * S::N; t += blockDim.x) {
+  for (int t = g; t < m * S::N; t += G) {
     const int k = t / S::N, j = t % S::N;
     uint32_t lam[8];
     if (staged) {
@@ -273,15 +299,24 @@ __global__ void __launch_bounds__(256) k_interp_endo(int ncomb, int m, const uin
       status[c] = hbl::HBL_DUPLICATE;
       continue;
     }
-    acc = jac_add(acc, S::term(pts + ((size_t)c * m + k) * S::WORDS, lam, j));
+    acc = jac_add(acc, S::term(pts + ((size_t)c * m + k) * S::WORDS, lam, j, chunk, nchunk));
   }
   sm[threadIdx.x] = acc;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) sm[threadIdx.x] = jac_add(sm[threadIdx.x], sm[threadIdx.x + s]);
+  for (int s = G / 2; s > 0; s >>= 1) {
+    if (g < s) sm[threadIdx.x] = jac_add(sm[threadIdx.x], sm[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) S::store(sm[0], out + (size_t)c * S::WORDS);
+  if (threadIdx.x == 0) {
+    // Horner over the chunk sums: R = sum_s 2^(s * bits) * S_s, one shared doubling tail
+    const int bits = 32 * S::DIGIT_WORDS / nchunk;
+    Jac<F> r = sm[(nchunk - 1) * G];
+    for (int s = nchunk - 2; s >= 0; s--) {
+      for (int b = 0; b < bits; b++) r = jac_dbl(r);
+      r = jac_add(r, sm[s * G]);
+    }
+    S::store(r, out + (size_t)c * S::WORDS);
+  }
 }
 
 // ------------------------------------------------------------------ SyncKeyGen
@@ -354,11 +389,21 @@ template <class F>
 static hipError_t combine(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out,
                           int* status) {
   if (ncomb <= 0) return hipSuccess;
-  int b = 64;  // power of two >= m * N (tree reduction), 64..256
-  while (b < 256 && b < m * hb::EndoSplit<F>::N) b *= 2;
+  using S = hb::EndoSplit<F>;
+  int g = 64;  // group: power of two >= m * N (tree reduction), 64..256
+  while (g < 256 && g < m * S::N) g *= 2;
+  // Latency mode (few combines: the chip is mostly idle, the serial chain is the time): split each
+  // digit into nchunk word-aligned chunks while the workgroup stays <= 256 threads.  Throughput
+  // mode (>= COMBINE_CHUNK_MAX combines fill the CUs): unsplit chains do the least total work
+  // (MI355X, 22 G2 shares: one combine 6.36 -> 5.37 ms chunked; 1,024 combines 83 k/s unsplit vs
+  // 49 k/s chunked).
+  constexpr int COMBINE_CHUNK_MAX = 128;
+  int nchunk = 1;
+  while (ncomb < COMBINE_CHUNK_MAX && nchunk < S::DIGIT_WORDS && g * nchunk * 2 <= 256) nchunk *= 2;
+  const int b = g * nchunk;
   const size_t lds = b * sizeof(hb::Jac<F>) + (m <= hb::LAM_LDS_MAX ? (size_t)m * 3 * sizeof(hb::Fr) : 0);
   hipLaunchKernelGGL(hb::k_interp_endo<F>, dim3((unsigned)ncomb), dim3(b), lds, s, ncomb, m, xs,
-                     (const uint32_t*)pts, (uint32_t*)out, status);
+                     (const uint32_t*)pts, (uint32_t*)out, status, nchunk);
   return hipGetLastError();
 }
 hipError_t combine_g1(hipStream_t s, int ncomb, int m, const uint32_t* xs, const void* pts, void* out, int* status) {

@@ -72,6 +72,31 @@ def test_interpolate_g2_n64_t21_matches_oracle(engine):
     assert cbls.combine_g2(t, idx[1], pts[1]) == (0, want)
 
 
+def test_interpolate_batched_unsplit_mode(engine):
+    """>= 128 combines per call take the throughput configuration of k_interp_endo (unsplit digit
+    chains); < 128 the latency configuration (chunked chains + Horner tail).  Both must give the
+    same group element: every (t+1)-subset of a degree-t key's shares interpolates to msk * H."""
+    rng = random.Random(130)
+    t = 21
+    coeffs = [rng.randrange(1, C.R) for _ in range(t + 1)]
+    h2 = cbls.g2_mul(G2, rng.randrange(1, C.R))
+    h1 = cbls.g1_mul(G1, rng.randrange(1, C.R))
+    s2 = [cbls.g2_mul(h2, tc.poly_eval(coeffs, i + 1)) for i in range(64)]
+    s1 = [cbls.g1_mul(h1, tc.poly_eval(coeffs, i + 1)) for i in range(64)]
+    subsets = [sorted(rng.sample(range(64), t + 1)) for _ in range(130)]
+    subsets[77] = [subsets[77][1]] + subsets[77][1:]  # duplicate entry in one combine
+    want2, want1 = cbls.g2_mul(h2, coeffs[0]), cbls.g1_mul(h1, coeffs[0])
+    for n in (130, 3):
+        out, st = engine.interpolate_g2(t, subsets[:n], [[s2[i] for i in sub] for sub in subsets[:n]])
+        assert [s for c, s in enumerate(st) if c != 77] == [0] * (n - (n > 77))
+        assert all(o == want2 for c, o in enumerate(out) if c != 77)
+        out, st = engine.interpolate_g1(t, subsets[:n], [[s1[i] for i in sub] for sub in subsets[:n]])
+        assert all(o == want1 for c, o in enumerate(out) if c != 77)
+    assert st == [0, 0, 0]
+    _, st = engine.interpolate_g2(t, subsets[:130], [[s2[i] for i in sub] for sub in subsets[:130]])
+    assert st[77] == 5
+
+
 def test_combine_verify_g2_matches_two_step(engine):
     """hbh_combine_verify_g2 (combine_and_verify_sig, src/threshold_sign.rs:249-270): same signature
     as interpolate_g2, master-key verdict as the C oracle's verify_g2; a wrong document hash gives
