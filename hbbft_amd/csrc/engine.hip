@@ -11,6 +11,7 @@
 
 #include "../../include/hbbft_hip.h"
 #include "launch.hpp"
+#include "wire.hpp"
 
 namespace {
 
@@ -539,6 +540,86 @@ int hbh_bivar_row(hbh_engine* e, size_t nrow, int t, size_t nparts, const uint8_
                            e->out_x.p));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, nout * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int hbh_g1_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (n == 0) return HBH_OK;
+  if (!in || !out || !ok) return fail(HBH_ERR_ARG, "null pointer");
+  if (n > (size_t)1 << 28) return fail(HBH_ERR_ARG, "batch too large");
+  // byte-level flag checks and the big-endian -> little-endian word reversal (pairing 0.14
+  // G1Compressed: 0x80 compressed, 0x40 infinity, 0x20 greatest y; infinity must be 0xc0 || 0^47)
+  std::vector<uint32_t> xw(n * 12);
+  std::vector<uint8_t> fl(n);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* b = in + i * 48;
+    uint8_t f = 0;
+    if (!(b[0] & 0x80)) {
+      f = hbl::WIRE_REJECT;
+    } else if (b[0] & 0x40) {
+      bool zero = (b[0] & 0x3f) == 0;
+      for (int k = 1; k < 48 && zero; k++) zero = b[k] == 0;
+      f = zero ? hbl::WIRE_INFINITY : hbl::WIRE_REJECT;
+    } else if (b[0] & 0x20) {
+      f = hbl::WIRE_GREATEST;
+    }
+    for (int w = 0; w < 12; w++) {
+      uint32_t v = 0;
+      for (int k = 0; k < 4; k++) {
+        const int pos = 47 - (w * 4 + k);  // little-endian byte w*4+k of x
+        v |= (uint32_t)(pos == 0 ? (b[0] & 0x1f) : b[pos]) << (8 * k);
+      }
+      xw[i * 12 + w] = v;
+    }
+    fl[i] = f;
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  HBH_CHECK(e->in_a.ensure(n * 48));
+  HBH_CHECK(e->in_b.ensure(n));
+  HBH_CHECK(e->out_x.ensure(n * HBH_G1_BYTES));
+  HBH_CHECK(e->out_v.ensure(n));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xw.data(), n * 48, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, fl.data(), n, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::g1_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, e->out_x.p,
+                               (uint8_t*)e->out_v.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(ok, e->out_v.p, n, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int hbh_commitment_eval(hbh_engine* e, size_t n, int t, size_t ncommits, const uint8_t* commits,
+                        const uint32_t* commit_idx, const uint32_t* xs, uint8_t* out) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (n == 0) return HBH_OK;
+  if (!commits || !commit_idx || !xs || !out) return fail(HBH_ERR_ARG, "null pointer");
+  if (n > (size_t)1 << 28) return fail(HBH_ERR_ARG, "batch too large");
+  for (size_t r = 0; r < n; r++)
+    if (commit_idx[r] >= ncommits) return fail(HBH_ERR_ARG, "commitment index out of range");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  const size_t cbytes = ncommits * (size_t)(t + 1) * HBH_G1_BYTES;
+  HBH_CHECK(e->in_a.ensure(cbytes));
+  HBH_CHECK(e->in_b.ensure(n * 4));
+  HBH_CHECK(e->in_c.ensure(n * 4));
+  HBH_CHECK(e->out_x.ensure(n * HBH_G1_BYTES));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, commits, cbytes, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, commit_idx, n * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_c.p, xs, n * 4, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::commit_eval(s, (int)n, t, e->in_a.p, (const uint32_t*)e->in_b.p, (const uint32_t*)e->in_c.p,
+                             e->out_x.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }

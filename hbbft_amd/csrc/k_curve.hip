@@ -367,6 +367,28 @@ __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint
   verdict[a] = jac_eq(acc, w) ? 1 : 0;
 }
 
+// Commitment::evaluate(x) = sum_j C_j x^j (threshold_crypto poly.rs) by Horner in G1 with the small
+// integer x -- PublicKeySet::public_key_share(i) = evaluate(i + 1), precomputed for every node by
+// NetworkInfo::new (src/network_info.rs:59-62).  commits holds ncommit commitments of t+1 points;
+// request r evaluates commitment commit_idx[r] at xs[r].  One thread per request.
+__global__ void __launch_bounds__(256) k_commit_eval(int n, int t, const uint32_t* __restrict__ commits,
+                                                     const uint32_t* __restrict__ commit_idx,
+                                                     const uint32_t* __restrict__ xs, uint32_t* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t* C = commits + (size_t)commit_idx[r] * (t + 1) * G1_WORDS;
+  const uint32_t x = xs[r];
+  Jac<Fp> acc = jac_zero<Fp>();
+  for (int j = t; j >= 0; j--) {
+    acc = jac_mul_small(acc, x);
+    Fp cx, cy;
+    bool inf;
+    load_g1(C + (size_t)j * G1_WORDS, cx, cy, inf);
+    if (!inf) acc = jac_add_affine(acc, cx, cy);
+  }
+  g1_jac_to_words(acc, out + (size_t)r * G1_WORDS);
+}
+
 }  // namespace hb
 
 // ------------------------------------------------------------------ host launchers
@@ -425,6 +447,14 @@ hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const u
   if (nack <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_bivar_check, grid_for(nack), dim3(256), 0, s, nack, t, (const uint32_t*)rows, row_idx, ys,
                      vals, verdict);
+  return hipGetLastError();
+}
+
+hipError_t commit_eval(hipStream_t s, int n, int t, const void* commits, const uint32_t* commit_idx, const uint32_t* xs,
+                       void* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_commit_eval, grid_for(n), dim3(256), 0, s, n, t, (const uint32_t*)commits, commit_idx, xs,
+                     (uint32_t*)out);
   return hipGetLastError();
 }
 

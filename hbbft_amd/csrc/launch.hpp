@@ -63,5 +63,8 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
 // check's part: verdict[a] = (sum_j R[row_idx[a]][j] * y^j == g1 * val[a]).
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
                        const uint32_t* vals, uint8_t* verdict);
+// Commitment::evaluate(x) for n (commitment, x) requests; commitments of t+1 G1 points.  out[r].
+hipError_t commit_eval(hipStream_t s, int n, int t, const void* commits, const uint32_t* commit_idx, const uint32_t* xs,
+                       void* out);
 
 }  // namespace hbl

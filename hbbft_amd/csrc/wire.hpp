@@ -1,0 +1,20 @@
+// Host launcher of the wire-format kernels (k_wire.hip).  Kept out of launch.hpp so that the
+// pairing translation units do not depend on it.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hbl {
+
+// per-point flags prepared by the host from the compressed encoding's top bits
+constexpr uint8_t WIRE_INFINITY = 1;  // valid encoding of the point at infinity
+constexpr uint8_t WIRE_GREATEST = 2;  // the "y is the larger root" bit
+constexpr uint8_t WIRE_REJECT = 4;    // malformed flags (not compressed, bad infinity encoding)
+
+// G1Compressed::into_affine for n points: xw = 12 canonical LE words of x per point (flag bits
+// cleared); out = ABI G1 points (all-zero when ok[i] == 0 or for infinity); ok[i] = 1 iff the
+// encoding decodes to a point of the prime-order subgroup.
+hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok);
+
+}  // namespace hbl

@@ -195,6 +195,34 @@ class Engine:
         return [[raw[(r * (t + 1) + i) * G1_BYTES:(r * (t + 1) + i + 1) * G1_BYTES] for i in range(t + 1)]
                 for r in range(nrow)]
 
+    def g1_decompress(self, encodings):
+        """pairing 0.14 G1Compressed::into_affine per 48-byte encoding: (ABI points, ok bytes)."""
+        b = _join(encodings, 48)
+        n = len(b) // 48
+        out = (ctypes.c_uint8 * max(n * G1_BYTES, 1))()
+        ok = (ctypes.c_uint8 * max(n, 1))()
+        keep = buf(b)
+        check(self._l.hbh_g1_decompress(self._h, n, keep[1], ctypes.cast(out, ctypes.c_void_p),
+                                        ctypes.cast(ok, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [raw[i * G1_BYTES:(i + 1) * G1_BYTES] for i in range(n)], bytes(ok)[:n]
+
+    def commitment_eval(self, t, commits, commit_idx, xs):
+        """Commitment::evaluate(x) per (commitment, x) request; public_key_share(i) = evaluate(i + 1)
+        as NetworkInfo::new precomputes it (src/network_info.rs:59-62)."""
+        if any(len(c) != t + 1 for c in commits):
+            raise ValueError("each commitment needs t+1 points")
+        cb = _join([p for c in commits for p in c], G1_BYTES)
+        n = len(xs)
+        ca, pca = _u32(commit_idx, n)
+        xa, pxa = _u32(xs, n)
+        out = (ctypes.c_uint8 * max(n * G1_BYTES, 1))()
+        keep = buf(cb)
+        check(self._l.hbh_commitment_eval(self._h, n, t, len(commits), keep[1], pca, pxa,
+                                          ctypes.cast(out, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [raw[r * G1_BYTES:(r + 1) * G1_BYTES] for r in range(n)]
+
     def bivar_ack_check(self, t, commits, part_idx, xs, ys, vals):
         """BivarCommitment::evaluate(x, y) == g1 * val (src/sync_key_gen.rs:542) per ack."""
         cb = _join([c for part in commits for c in part], G1_BYTES)

@@ -142,6 +142,25 @@ int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, cons
                         const uint32_t* part_idx, const uint32_t* xs, const uint32_t* ys, const uint8_t* vals,
                         uint8_t* verdicts);
 
+/* Commitment::evaluate(x) = sum_j C_j x^j for n (commitment, x) requests; commits holds ncommits
+ * Commitments of t+1 G1 points each, out = n G1 points.  PublicKeySet::public_key_share(i) is
+ * evaluate(i + 1): NetworkInfo::new precomputes it for every node (src/network_info.rs:59-62), and
+ * a SyncKeyGen node does the same for the generated key (src/sync_key_gen.rs:449 via
+ * PublicKeySet::from(commit)).  xs are the 1-based integers the reference passes. */
+int hbh_commitment_eval(hbh_engine* eng, size_t n, int t, size_t ncommits, const uint8_t* commits,
+                        const uint32_t* commit_idx, const uint32_t* xs, uint8_t* out);
+
+/* ---------------------------------------------------------------- wire formats
+ * pairing 0.14 G1Compressed::into_affine for n 48-byte compressed G1 points (zcash encoding:
+ * big-endian x, 0x80 = compressed, 0x40 = infinity, 0x20 = larger y).  out[i] = the ABI point,
+ * ok[i] = 1 iff the encoding is well formed, x < p, x^3 + 4 is a square and the point lies in the
+ * prime-order subgroup -- the checks threshold_crypto's deserialisation runs on every PublicKey,
+ * PublicKeyShare, DecryptionShare and Ciphertext U before it reaches the verify calls (serde
+ * decoding of hbbft's messages; decode sites listed in SURVEY §8f f2).
+ * A point with ok[i] == 0 is written as all-zero bytes; the caller rejects the message as the
+ * reference's deserialisation error does. */
+int hbh_g1_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok);
+
 /* ---------------------------------------------------------------- implementation selection
  * Three pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks
  * them): HBH_IMPL_THREAD (one thread per check, 14x28-bit unsigned limbs, k_pairing.hip),

@@ -216,3 +216,71 @@ def test_bivar_t33_matches_oracle(engine):
     vals[3] = (vals[3] + 1) % C.R  # a tampered Ack value
     v = engine.bivar_ack_check(t, parts, pidx, [x] * len(ys), ys, vals)
     assert list(v) == [1, 1, 1, 0, 1, 1]
+
+
+def test_commitment_eval_public_key_shares(engine):
+    """Commitment::evaluate(i + 1) = PublicKeySet::public_key_share(i) (src/network_info.rs:59-62):
+    the golden fixture's key set (re-derived from its recorded seed, as gen_golden.py draws it) must
+    give the fixture's public key shares; random commitments with an infinity coefficient and
+    x = 0 (= C_0) match the C oracle."""
+    d = load("threshold_sign_n10_t3.json")
+    rng = random.Random(d["seed"])
+    coeffs = [rng.randrange(1, C.R) for _ in range(d["t"] + 1)]
+    commit = [cbls.g1_mul(G1, c) for c in coeffs]
+    got = engine.commitment_eval(d["t"], [commit], [0] * d["n"], [i + 1 for i in range(d["n"])])
+    assert got == [g1a(bytes.fromhex(p)) for p in d["pk_shares"]]
+    master = engine.commitment_eval(d["t"], [commit], [0], [0])[0]
+    assert master == g1a(C.g1_uncompressed(C.g1_decompress(bytes.fromhex(d["master_pk"]))))
+    r2 = random.Random(33)
+    t = 33
+    polys = [[r2.randrange(1, C.R) for _ in range(t + 1)] for _ in range(3)]
+    polys[1][5] = 0  # infinity coefficient
+    commits = [[cbls.g1_mul(G1, c) for c in p] for p in polys]
+    reqs = [(c, x) for c in range(3) for x in (0, 1, 2, 64, 100, 0xFFFFFFFF)]
+    got = engine.commitment_eval(t, commits, [c for c, _ in reqs], [x for _, x in reqs])
+    assert got == [cbls.g1_mul(G1, tc.poly_eval(polys[c], x)) for c, x in reqs]
+
+
+def test_g1_decompress_matches_oracle(engine):
+    """hbh_g1_decompress = pairing 0.14 G1Compressed::into_affine (SURVEY §8f f2): valid points
+    (both y signs), infinity, malformed flags, x >= p, x off the curve, and on-curve points outside
+    the prime-order subgroup -- accept/reject and decoded bytes equal the oracle's."""
+    rng = random.Random(48)
+    encs = []
+    for _ in range(24):
+        encs.append(C.g1_compress(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))))
+    encs.append(C.g1_compress(None))                       # infinity
+    encs.append(bytes([0xC0]) + bytes(46) + b"\x01")       # bad infinity
+    encs.append(bytes([0x00]) + encs[0][1:])                # not compressed
+    encs.append(bytes([encs[1][0] ^ 0x20]) + encs[1][1:])   # other root: valid, negated point
+    pb = (C.P + 5).to_bytes(48, "big")
+    encs.append(bytes([pb[0] | 0x80]) + pb[1:])             # x >= p
+    off, cof = 0, 0
+    while off < 3 or cof < 3:                               # off-curve x / on-curve non-subgroup x
+        x = rng.randrange(C.P)
+        b = x.to_bytes(48, "big")
+        e = bytes([b[0] | 0x80 | (0x20 if rng.random() < 0.5 else 0)]) + b[1:]
+        try:
+            C.g1_decompress(e)
+            continue
+        except C.DecodeError as err:
+            kind = str(err)
+        if "curve" in kind and off < 3:
+            off += 1
+            encs.append(e)
+        elif "subgroup" in kind and cof < 3:
+            cof += 1
+            encs.append(e)
+    want_pts, want_ok = [], []
+    for e in encs:
+        try:
+            pt = C.g1_decompress(e)
+            want_pts.append(bytes(96) if pt is None else g1a(C.g1_uncompressed(pt)))
+            want_ok.append(1)
+        except C.DecodeError:
+            want_pts.append(bytes(96))
+            want_ok.append(0)
+    got, ok = engine.g1_decompress(encs)
+    assert list(ok) == want_ok
+    assert got == want_pts
+    assert sum(want_ok) == 26 and len(encs) == 35
