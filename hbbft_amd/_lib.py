@@ -37,6 +37,7 @@ SIGNATURES = [
     ("hbh_g2_mul", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_bivar_row", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),
     ("hbh_g1_decompress", _I, [_P, _SZ, _P, _P, _P]),
+    ("hbh_g2_decompress", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_commitment_eval", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),
     ("hbh_bivar_ack_check", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P, _P, _P]),
     ("hbh_engine_set_pairing_impl", _I, [_P, _I]),

@@ -544,54 +544,79 @@ int hbh_bivar_row(hbh_engine* e, size_t nrow, int t, size_t nparts, const uint8_
   return HBH_OK;
 }
 
-int hbh_g1_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok) {
+}  // extern "C"
+
+namespace {
+// Byte-level half of pairing 0.14's compressed decoding: flags (0x80 compressed, 0x40 infinity --
+// then 0xc0 || 0...0 exactly --, 0x20 larger y) and the big-endian -> little-endian word reversal.
+// The encoding holds nfe 48-byte field elements, highest Fp2 coefficient first (G2: x.c1 || x.c0);
+// words come out as coefficient 0 first (12 words each).
+void parse_compressed(const uint8_t* b, int nfe, uint32_t* words, uint8_t& f) {
+  f = 0;
+  if (!(b[0] & 0x80)) {
+    f = hbl::WIRE_REJECT;
+  } else if (b[0] & 0x40) {
+    bool zero = (b[0] & 0x3f) == 0;
+    for (int k = 1; k < 48 * nfe && zero; k++) zero = b[k] == 0;
+    f = zero ? hbl::WIRE_INFINITY : hbl::WIRE_REJECT;
+  } else if (b[0] & 0x20) {
+    f = hbl::WIRE_GREATEST;
+  }
+  for (int c = 0; c < nfe; c++) {
+    const uint8_t* e = b + 48 * (nfe - 1 - c);
+    for (int w = 0; w < 12; w++) {
+      uint32_t v = 0;
+      for (int k = 0; k < 4; k++) {
+        const int pos = 47 - (w * 4 + k);  // little-endian byte w*4+k of the element
+        const uint8_t byte = (e == b && pos == 0) ? (uint8_t)(b[0] & 0x1f) : e[pos];
+        v |= (uint32_t)byte << (8 * k);
+      }
+      words[c * 12 + w] = v;
+    }
+  }
+}
+
+int run_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok, bool g2) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
   if (n == 0) return HBH_OK;
   if (!in || !out || !ok) return fail(HBH_ERR_ARG, "null pointer");
   if (n > (size_t)1 << 28) return fail(HBH_ERR_ARG, "batch too large");
-  // byte-level flag checks and the big-endian -> little-endian word reversal (pairing 0.14
-  // G1Compressed: 0x80 compressed, 0x40 infinity, 0x20 greatest y; infinity must be 0xc0 || 0^47)
-  std::vector<uint32_t> xw(n * 12);
+  const int nfe = g2 ? 2 : 1;
+  const size_t pb = g2 ? HBH_G2_BYTES : HBH_G1_BYTES;
+  std::vector<uint32_t> xw(n * 12 * nfe);
   std::vector<uint8_t> fl(n);
-  for (size_t i = 0; i < n; i++) {
-    const uint8_t* b = in + i * 48;
-    uint8_t f = 0;
-    if (!(b[0] & 0x80)) {
-      f = hbl::WIRE_REJECT;
-    } else if (b[0] & 0x40) {
-      bool zero = (b[0] & 0x3f) == 0;
-      for (int k = 1; k < 48 && zero; k++) zero = b[k] == 0;
-      f = zero ? hbl::WIRE_INFINITY : hbl::WIRE_REJECT;
-    } else if (b[0] & 0x20) {
-      f = hbl::WIRE_GREATEST;
-    }
-    for (int w = 0; w < 12; w++) {
-      uint32_t v = 0;
-      for (int k = 0; k < 4; k++) {
-        const int pos = 47 - (w * 4 + k);  // little-endian byte w*4+k of x
-        v |= (uint32_t)(pos == 0 ? (b[0] & 0x1f) : b[pos]) << (8 * k);
-      }
-      xw[i * 12 + w] = v;
-    }
-    fl[i] = f;
-  }
+  for (size_t i = 0; i < n; i++) parse_compressed(in + i * 48 * nfe, nfe, xw.data() + i * 12 * nfe, fl[i]);
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
-  HBH_CHECK(e->in_a.ensure(n * 48));
+  HBH_CHECK(e->in_a.ensure(xw.size() * 4));
   HBH_CHECK(e->in_b.ensure(n));
-  HBH_CHECK(e->out_x.ensure(n * HBH_G1_BYTES));
+  HBH_CHECK(e->out_x.ensure(n * pb));
   HBH_CHECK(e->out_v.ensure(n));
-  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xw.data(), n * 48, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xw.data(), xw.size() * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_b.p, fl.data(), n, hipMemcpyHostToDevice, s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::g1_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, e->out_x.p,
-                               (uint8_t*)e->out_v.p));
+  if (g2)
+    HBH_CHECK(hbl::g2_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, e->out_x.p,
+                                 (uint8_t*)e->out_v.p));
+  else
+    HBH_CHECK(hbl::g1_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, e->out_x.p,
+                                 (uint8_t*)e->out_v.p));
   e->timer.end(s, tm);
-  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * pb, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipMemcpyAsync(ok, e->out_v.p, n, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int hbh_g1_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok) {
+  return run_decompress(e, n, in, out, ok, false);
+}
+int hbh_g2_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok) {
+  return run_decompress(e, n, in, out, ok, true);
 }
 
 int hbh_commitment_eval(hbh_engine* e, size_t n, int t, size_t ncommits, const uint8_t* commits,

@@ -1,6 +1,7 @@
-// Wire-format parsing on the GPU: pairing 0.14 G1Compressed::into_affine for
-// batches of 48-byte compressed G1 points (public keys, decryption shares, ciphertext U) -- the
-// square root that recovers y, the sign choice and the prime-order-subgroup check.  The host does
+// Wire-format parsing on the GPU: pairing 0.14 G1Compressed / G2Compressed
+// ::into_affine for batches of compressed points (public keys, decryption shares, ciphertext U in
+// G1; signature shares, signatures, ciphertext W in G2) -- the square root that recovers y, the
+// sign choice and the prime-order-subgroup check.  The host does
 // the byte-level flag checks and the big-endian -> little-endian word reversal (wire.hpp).
 #include <hip/hip_runtime.h>
 
@@ -81,6 +82,101 @@ __global__ void __launch_bounds__(256) k_g1_decompress(int n, const uint32_t* __
   ok[i] = valid ? 1 : 0;
 }
 
+// pairing 0.14 Ord for Fq2: c1 first, then c0 (canonical integers)
+__device__ __forceinline__ bool f2_gt_canon(const Fp2& a, const Fp2& b) {
+  uint32_t a0[12], a1[12], b0[12], b1[12];
+  fp_to_words(a.c0, a0);
+  fp_to_words(a.c1, a1);
+  fp_to_words(b.c0, b0);
+  fp_to_words(b.c1, b1);
+  bool eq1 = true;
+  for (int k = 0; k < 12; k++) eq1 = eq1 && a1[k] == b1[k];
+  return eq1 ? words_gt(a0, b0, 12) : words_gt(a1, b1, 12);
+}
+
+__device__ __forceinline__ Fp2 f2_pow_words(const Fp2& a, const uint32_t e[12]) {
+  Fp2 r = f2_one();
+  for (int i = 12 * 32 - 1; i >= 0; i--) {
+    r = f2_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1) r = f2_mul(r, a);
+  }
+  return r;
+}
+
+__device__ __forceinline__ bool f2_is_minus_one(const Fp2& a) {
+  return fp_eq(a.c0, fp_neg(fp_one())) && fp_is_zero(a.c1);
+}
+
+// square root in Fp2 for p = 3 mod 4 (Adj / Rodriguez-Henriquez): false when a is not a square
+__device__ __forceinline__ bool f2_sqrt(const Fp2& a, Fp2& out) {
+  if (f2_is_zero(a)) {
+    out = f2_zero();
+    return true;
+  }
+  uint32_t e[12];
+  for (int i = 0; i < 12; i++) e[i] = PM2_W[i];
+  e[0] -= 1;  // p - 3 (no borrow: the low word of p - 2 is 0xffffaaa9)
+  for (int i = 0; i < 12; i++) e[i] = (e[i] >> 2) | (i < 11 ? (e[i + 1] << 30) : 0u);  // (p - 3) / 4
+  const Fp2 a1 = f2_pow_words(a, e);
+  const Fp2 alpha = f2_mul(f2_sqr(a1), a);
+  const Fp2 a0 = f2_mul(f2_conj(alpha), alpha);  // alpha^p * alpha
+  if (f2_is_minus_one(a0)) return false;
+  const Fp2 x0 = f2_mul(a1, a);
+  Fp2 res;
+  if (f2_is_minus_one(alpha)) {
+    res = {fp_neg(x0.c1), x0.c0};  // x0 * u
+  } else {
+    uint32_t h[12];
+    for (int i = 0; i < 12; i++) h[i] = PM2_W[i];
+    h[0] += 1;  // p - 1
+    for (int i = 0; i < 12; i++) h[i] = (h[i] >> 1) | (i < 11 ? (h[i + 1] << 31) : 0u);  // (p - 1) / 2
+    res = f2_mul(f2_pow_words(f2_add(f2_one(), alpha), h), x0);
+  }
+  const Fp2 chk = f2_sub(f2_sqr(res), a);
+  out = res;
+  return f2_is_zero(chk);
+}
+
+__global__ void __launch_bounds__(256) k_g2_decompress(int n, const uint32_t* __restrict__ xw,
+                                                       const uint8_t* __restrict__ flags, uint32_t* __restrict__ out,
+                                                       uint8_t* __restrict__ ok) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t* o = out + (size_t)i * G2_WORDS;
+  const uint8_t f = flags[i];
+  bool valid = false;
+  uint32_t x[24], y[24];
+  for (int k = 0; k < 24; k++) x[k] = xw[(size_t)i * 24 + k], y[k] = 0;
+  if (f & hbl::WIRE_INFINITY) {
+    valid = true;
+    for (int k = 0; k < 24; k++) x[k] = 0;
+  } else if (!(f & hbl::WIRE_REJECT)) {
+    uint32_t p[12];
+    for (int k = 0; k < 12; k++) p[k] = PM2_W[k];
+    p[0] += 2;
+    if (words_gt(p, x, 12) && words_gt(p, x + 12, 12)) {
+      const Fp2 xm = {fp_from_words(x), fp_from_words(x + 12)};
+      const Fp2 b2 = {fp_const(B1_M), fp_const(B1_M)};  // 4 (1 + u)
+      const Fp2 rhs = f2_add(f2_mul(f2_sqr(xm), xm), b2);
+      Fp2 ym;
+      if (f2_sqrt(rhs, ym)) {
+        const Fp2 ny = f2_neg(ym);
+        if (f2_gt_canon(ym, ny) != ((f & hbl::WIRE_GREATEST) != 0)) ym = ny;
+        fp_to_words(ym.c0, y);
+        fp_to_words(ym.c1, y + 12);
+        uint32_t r[8];
+        for (int k = 0; k < 8; k++) r[k] = FR_W[k];
+        valid = jac_is_zero(jac_mul_affine(xm, ym, false, r));
+      }
+    }
+  }
+  for (int k = 0; k < 24; k++) {
+    o[k] = valid ? x[k] : 0u;
+    o[24 + k] = valid ? y[k] : 0u;
+  }
+  ok[i] = valid ? 1 : 0;
+}
+
 }  // namespace hb
 
 namespace hbl {
@@ -88,6 +184,13 @@ namespace hbl {
 hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_g1_decompress, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, xw, flags,
+                     (uint32_t*)out, ok);
+  return hipGetLastError();
+}
+
+hipError_t g2_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_g2_decompress, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, xw, flags,
                      (uint32_t*)out, ok);
   return hipGetLastError();
 }

@@ -16,5 +16,7 @@ constexpr uint8_t WIRE_REJECT = 4;    // malformed flags (not compressed, bad in
 // cleared); out = ABI G1 points (all-zero when ok[i] == 0 or for infinity); ok[i] = 1 iff the
 // encoding decodes to a point of the prime-order subgroup.
 hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok);
+// G2Compressed::into_affine: xw = 24 words per point (x.c0 then x.c1), out = ABI G2 points.
+hipError_t g2_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok);
 
 }  // namespace hbl

@@ -195,17 +195,23 @@ class Engine:
         return [[raw[(r * (t + 1) + i) * G1_BYTES:(r * (t + 1) + i + 1) * G1_BYTES] for i in range(t + 1)]
                 for r in range(nrow)]
 
-    def g1_decompress(self, encodings):
-        """pairing 0.14 G1Compressed::into_affine per 48-byte encoding: (ABI points, ok bytes)."""
-        b = _join(encodings, 48)
-        n = len(b) // 48
-        out = (ctypes.c_uint8 * max(n * G1_BYTES, 1))()
+    def _decompress(self, fn, enc_size, pt_size, encodings):
+        b = _join(encodings, enc_size)
+        n = len(b) // enc_size
+        out = (ctypes.c_uint8 * max(n * pt_size, 1))()
         ok = (ctypes.c_uint8 * max(n, 1))()
         keep = buf(b)
-        check(self._l.hbh_g1_decompress(self._h, n, keep[1], ctypes.cast(out, ctypes.c_void_p),
-                                        ctypes.cast(ok, ctypes.c_void_p)))
+        check(fn(self._h, n, keep[1], ctypes.cast(out, ctypes.c_void_p), ctypes.cast(ok, ctypes.c_void_p)))
         raw = bytes(out)
-        return [raw[i * G1_BYTES:(i + 1) * G1_BYTES] for i in range(n)], bytes(ok)[:n]
+        return [raw[i * pt_size:(i + 1) * pt_size] for i in range(n)], bytes(ok)[:n]
+
+    def g1_decompress(self, encodings):
+        """pairing 0.14 G1Compressed::into_affine per 48-byte encoding: (ABI points, ok bytes)."""
+        return self._decompress(self._l.hbh_g1_decompress, 48, G1_BYTES, encodings)
+
+    def g2_decompress(self, encodings):
+        """pairing 0.14 G2Compressed::into_affine per 96-byte encoding: (ABI points, ok bytes)."""
+        return self._decompress(self._l.hbh_g2_decompress, 96, G2_BYTES, encodings)
 
     def commitment_eval(self, t, commits, commit_idx, xs):
         """Commitment::evaluate(x) per (commitment, x) request; public_key_share(i) = evaluate(i + 1)

@@ -160,6 +160,10 @@ int hbh_commitment_eval(hbh_engine* eng, size_t n, int t, size_t ncommits, const
  * A point with ok[i] == 0 is written as all-zero bytes; the caller rejects the message as the
  * reference's deserialisation error does. */
 int hbh_g1_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok);
+/* G2Compressed::into_affine for n 96-byte compressed G2 points (x.c1 || x.c0 big-endian, flags in
+ * the first byte; y^2 = x^3 + 4(1 + u); larger y by pairing 0.14's Fq2 order: c1, then c0);
+ * out = ABI G2 points.  Same ok / all-zero convention as hbh_g1_decompress. */
+int hbh_g2_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok);
 
 /* ---------------------------------------------------------------- implementation selection
  * Three pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks

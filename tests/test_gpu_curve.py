@@ -284,3 +284,45 @@ def test_g1_decompress_matches_oracle(engine):
     assert list(ok) == want_ok
     assert got == want_pts
     assert sum(want_ok) == 26 and len(encs) == 35
+
+
+def test_g2_decompress_matches_oracle(engine):
+    """hbh_g2_decompress = pairing 0.14 G2Compressed::into_affine (SURVEY §8f f2): Fp2 square
+    root, the c1-then-c0 root order, and the subgroup check, against the oracle."""
+    rng = random.Random(96)
+    encs = [C.g2_compress(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R))) for _ in range(8)]
+    encs.append(C.g2_compress(None))                                   # infinity
+    encs.append(bytes([0xC0]) + bytes(94) + b"\x02")                   # bad infinity
+    encs.append(bytes([encs[0][0] & 0x7F]) + encs[0][1:])               # not compressed
+    encs.append(bytes([encs[1][0] ^ 0x20]) + encs[1][1:])               # other root
+    pb = (C.P + 1).to_bytes(48, "big")
+    encs.append(encs[2][:48] + pb)                                      # x.c0 >= p
+    encs.append(bytes([pb[0] | 0x80]) + pb[1:] + encs[2][48:])           # x.c1 >= p
+    off, cof = 0, 0
+    while off < 2 or cof < 2:
+        b = rng.randrange(C.P).to_bytes(48, "big") + rng.randrange(C.P).to_bytes(48, "big")
+        e = bytes([b[0] | 0x80 | (0x20 if rng.random() < 0.5 else 0)]) + b[1:]
+        try:
+            C.g2_decompress(e)
+            continue
+        except C.DecodeError as err:
+            kind = str(err)
+        if "curve" in kind and off < 2:
+            off += 1
+            encs.append(e)
+        elif "subgroup" in kind and cof < 2:
+            cof += 1
+            encs.append(e)
+    want_pts, want_ok = [], []
+    for e in encs:
+        try:
+            pt = C.g2_decompress(e)
+            want_pts.append(bytes(192) if pt is None else g2a(C.g2_uncompressed(pt)))
+            want_ok.append(1)
+        except C.DecodeError:
+            want_pts.append(bytes(192))
+            want_ok.append(0)
+    got, ok = engine.g2_decompress(encs)
+    assert list(ok) == want_ok
+    assert got == want_pts
+    assert sum(want_ok) == 10 and len(encs) == 18
