@@ -176,6 +176,40 @@ def combine_latency(eng, w, reps=7):
     return statistics.median(times), ndocs / bt, ndocs / (dev_ms / 1e3)
 
 
+P_FIELD = int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16)
+
+
+def g2_compress_abi(b):
+    """ABI G2 point -> the reference's 96-byte compressed wire encoding (pairing 0.14 G2Compressed:
+    x.c1 || x.c0 big-endian, 0x80 compressed, 0x40 infinity, 0x20 larger y in Fq2 order c1, c0)."""
+    if not any(b):
+        return bytes([0xC0]) + bytes(95)
+    x0, x1, y0, y1 = (int.from_bytes(b[o:o + 48], "little") for o in (0, 48, 96, 144))
+    n0, n1 = (P_FIELD - y0) % P_FIELD, (P_FIELD - y1) % P_FIELD
+    greatest = y1 > n1 if y1 != n1 else y0 > n0
+    e = bytearray(x1.to_bytes(48, "big") + x0.to_bytes(48, "big"))
+    e[0] |= 0x80 | (0x20 if greatest else 0)
+    return bytes(e)
+
+
+def decode_rate(eng, w, n):
+    """Wire decoding of the batch's n signature shares: hbh_g2_decompress rate
+    host-to-host (PCIe + host flag parsing included) and device-only; decoded bytes must equal the
+    shares the workload generated."""
+    from hbbft_amd._lib import STAGE_CURVE
+    sig = w.sig_batch[:n * 192]
+    encs = b"".join(g2_compress_abi(sig[i * 192:(i + 1) * 192]) for i in range(n))
+    eng.g2_decompress(encs[:96 * 64])  # warm-up
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    pts, ok = eng.g2_decompress(encs)
+    host_s = time.perf_counter() - t0
+    dev_ms = eng.stage_time(STAGE_CURVE)[0]
+    eng.set_profiling(False)
+    assert all(ok) and b"".join(pts) == sig, "G2 decoding differs from the generated shares"
+    return n / host_s, n / (dev_ms / 1e3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -284,6 +318,9 @@ def main():
             out["combine_latency_ms"] = lat
             out["combines_per_s_batched"] = rate          # host-to-host, 1,024 combines in one call
             out["combines_per_s_batched_device"] = dev_rate  # k_interp_endo time only
+            dec_host, dec_dev = decode_rate(eng, w, n)
+            out["g2_decode_per_s"] = dec_host            # hbh_g2_decompress, host-to-host
+            out["g2_decode_per_s_device"] = dec_dev      # k_g2_decompress time only
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(w)
         print(json.dumps(out), flush=True)
