@@ -86,6 +86,14 @@ class Engine:
                                             pdi, ctypes.cast(out, ctypes.c_void_p)))
         return bytes(out)[:n]
 
+    def verify_signatures(self, pks, sigs, hashes):
+        """PublicKey::verify(sig, msg) batch with H = hash_g2(msg) hashed on the host: DHB signed
+        votes (src/dynamic_honey_badger/votes.rs:153-158) and key-gen messages
+        (src/dynamic_honey_badger/dynamic_honey_badger.rs:514-526).  Same pairing-equality check as
+        verify_sig_shares, one hash per item."""
+        n = len(_join(pks, G1_BYTES)) // G1_BYTES
+        return self.verify_sig_shares(pks, sigs, hashes, list(range(n)))
+
     def verify_dec_shares(self, shares, pks, huv, w, ct_idx):
         """PublicKeyShare::verify_decryption_share batch (src/threshold_decrypt.rs:220-229)."""
         sb, pkb = _join(shares, G1_BYTES), _join(pks, G1_BYTES)

@@ -63,6 +63,8 @@ int hbh_device_count(int* out);
  * Replaces every pairing comparison on the path:
  *   PublicKeyShare::verify_g2   (src/threshold_sign.rs:223)   P1=pk_i, Q1=H, P2=g1, Q2=sig_i
  *   PublicKey::verify_g2        (src/threshold_sign.rs:264)   P1=pk,   Q1=H, P2=g1, Q2=sig
+ *   PublicKey::verify (signed votes / key-gen messages, src/dynamic_honey_badger/votes.rs:157,
+ *     dynamic_honey_badger.rs:520)                                P1=pk,   Q1=hash_g2(msg), P2=g1, Q2=sig
  *   Ciphertext::verify          (src/threshold_decrypt.rs:142) P1=g1, Q1=W, P2=U, Q2=H_uv
  *   verify_decryption_share     (src/threshold_decrypt.rs:227) P1=D_i, Q1=H_uv, P2=pk_i, Q2=W
  */

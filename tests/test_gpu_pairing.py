@@ -130,3 +130,25 @@ def test_lane_coop_matches_thread_random_batch(engine):
     for i, w in want:
         assert v1[i] == int(w), i
     assert sum(v1) == sum(1 for i in range(n) if i % 11 not in (3, 5))
+
+
+def test_verify_signatures_public_key_verify(eng):
+    """PublicKey::verify for DHB signed votes / key-gen messages (votes.rs:153-158,
+    dynamic_honey_badger.rs:514-526): valid, wrong message, wrong key, pk = sig = O (verifies:
+    pairing with O is 1) -- verdicts equal the C oracle's."""
+    import random
+    from oracle import cbls
+    rng = random.Random(157)
+    G1 = g1a(C.g1_uncompressed(C.G1_GEN))
+    G2 = g2a(C.g2_uncompressed(C.G2_GEN))
+    sks = [rng.randrange(1, C.R) for _ in range(4)]
+    pks = [cbls.g1_mul(G1, k) for k in sks]
+    hs = [cbls.g2_mul(G2, rng.randrange(1, C.R)) for _ in range(4)]
+    sigs = [cbls.g2_mul(h, k) for h, k in zip(hs, sks)]
+    items = [(pks[0], sigs[0], hs[0]), (pks[1], sigs[1], hs[1]),
+             (pks[2], sigs[2], hs[3]),          # signature of another message
+             (pks[3], sigs[2], hs[2]),          # another voter's key
+             (bytes(96), bytes(192), hs[0])]    # pk = O, sig = O
+    got = eng.verify_signatures([a for a, _, _ in items], [b for _, b, _ in items], [c for _, _, c in items])
+    want = [int(cbls.verify_g2(a, b, c)) for a, b, c in items]
+    assert list(got) == want == [1, 1, 0, 0, 1]
