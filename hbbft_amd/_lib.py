@@ -45,7 +45,7 @@ SIGNATURES = [
     ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
-IMPL_THREAD, IMPL_LANE_COOP, IMPL_THREAD_SIGNED, IMPL_AUTO = 0, 1, 2, 3
+IMPL_LANE_COOP, IMPL_THREAD_SIGNED, IMPL_AUTO, IMPL_PAIR = 1, 2, 3, 4   # HBH_IMPL_* (0 = retired THREAD)
 
 _lib = None
 

@@ -86,8 +86,13 @@ struct hbh_engine {
   bool profiling = false;
   int impl = HBH_IMPL_AUTO;  // pairing implementation (hbh_engine_set_pairing_impl)
   StageTimer timer;
+  // Completion of the last call's device work on whichever stream it ran.  Every call waits for it
+  // on its own stream before touching the engine-owned workspaces, so a _dev call on a caller
+  // stream can never overwrite tables another stream's kernels are still reading.
+  hipEvent_t done = nullptr;
   // workspaces
-  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3;
+  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep;
+  size_t g1rep_n = 0;
   // staging for host-pointer entry points
   DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
 };
@@ -95,6 +100,19 @@ struct hbh_engine {
 namespace {
 
 using hbl::line_table_bytes;
+
+// Start of a call on stream s: order it after the engine's previous call.
+int begin_call(hbh_engine* e, hipStream_t s) {
+  HBH_CHECK(hipStreamWaitEvent(s, e->done, 0));
+  return HBH_OK;
+}
+int end_call(hbh_engine* e, hipStream_t s) {
+  HBH_CHECK(hipEventRecord(e->done, s));
+  return HBH_OK;
+}
+
+// n copies of the G1 generator on the device, for the implementations that read P per check
+int g1_repeated(hbh_engine* e, hipStream_t s, size_t n, const void** out);
 
 // Line tables for up to two G2 point sets, in one launch.
 int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, DevBuf& coef0, DevBuf& inf0,
@@ -115,45 +133,76 @@ int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, 
   return HBH_OK;
 }
 
-int launch_pairing(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, size_t nq1, const uint32_t* d_i1,
-                   const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v, uint32_t* d_value);
+int resolve_impl(const hbh_engine* e, size_t n) {
+  if (e->impl != HBH_IMPL_AUTO) return e->impl;
+  return n < HBH_AUTO_LANE_COOP_MAX ? HBH_IMPL_LANE_COOP : HBH_IMPL_PAIR;
+}
 
-int run_pairing_eq_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
-                       const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2,
-                       uint8_t* d_v) {
-  if (n == 0) return HBH_OK;
-  if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
-  int rc = launch_prepare(e, s, d_q1, nq1, e->coef1, e->inf1, d_q2, nq2, &e->coef2, &e->inf2);
-  if (rc) return rc;
-  return launch_pairing(e, s, n, d_p1, nq1, d_i1, d_p2, nq2, d_i2, 1, d_v, nullptr);
+// HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
+// table (k_pair_prep); every other side is walked inside the verify kernel.
+int launch_pair(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
+                const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2, int flags,
+                uint8_t* d_v, uint32_t* d_value) {
+  hbl::PairSideDesc sd[2] = {{d_p1, d_q1, nullptr, nullptr, d_i1, nq1}, {d_p2, d_q2, nullptr, nullptr, d_i2, nq2}};
+  DevBuf* tab[2] = {&e->coef1, &e->coef2};
+  DevBuf* inf[2] = {&e->inf1, &e->inf2};
+  for (int k = 0; k < 2; k++) {
+    if (!sd[k].idx || sd[k].nq * 4 > n) continue;
+    HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
+    HBH_CHECK(inf[k]->ensure(sd[k].nq));
+    hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
+    HBH_CHECK(hbl::pair_prep(s, (int)sd[k].nq, sd[k].q, tab[k]->p, (uint8_t*)inf[k]->p));
+    e->timer.end(s, t);
+    sd[k].lines = tab[k]->p;
+    sd[k].qinf = (const uint8_t*)inf[k]->p;
+  }
+  hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
+  HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  e->timer.end(s, t);
+  return HBH_OK;
 }
 
 // multi-Miller loop + final exponentiation over prepared tables (coef1/2, inf1/2)
-int launch_pairing(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, size_t nq1, const uint32_t* d_i1,
-                   const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v, uint32_t* d_value) {
+int launch_prepared(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_p1, size_t nq1,
+                    const uint32_t* d_i1, const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v,
+                    uint32_t* d_value) {
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  int impl = e->impl;
-  if (impl == HBH_IMPL_AUTO) impl = n < HBH_AUTO_LANE_COOP_MAX ? HBH_IMPL_LANE_COOP : HBH_IMPL_THREAD_SIGNED;
   if (impl == HBH_IMPL_THREAD_SIGNED) {
     const size_t bytes = hbl::ts_state_bytes((int)n);
     for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
     HBH_CHECK(hbl::ts_miller(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2, e->coef2.p,
                              (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, e->lc0.p));
     HBH_CHECK(hbl::ts_final_exp(s, (int)n, e->lc0.p, e->lc1.p, e->lc2.p, e->lc3.p, d_v, d_value));
-  } else if (impl == HBH_IMPL_LANE_COOP) {
+  } else {
     const size_t bytes = hbl::lc_state_words((int)n) * sizeof(int32_t);
     for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
     HBH_CHECK(hbl::lc_pairing(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
                               e->coef2.p, (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, (int32_t*)e->lc0.p,
                               (int32_t*)e->lc1.p, (int32_t*)e->lc2.p, (int32_t*)e->lc3.p, d_v, d_value));
-  } else if (d_value) {
-    HBH_CHECK(hbl::pairing_value(s, (int)n, d_p1, e->coef1.p, (const uint8_t*)e->inf1.p, d_value));
-  } else {
-    HBH_CHECK(hbl::pairing_eq(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
-                              e->coef2.p, (int)nq2, (const uint8_t*)e->inf2.p, d_i2, d_v));
   }
   e->timer.end(s, t);
   return HBH_OK;
+}
+
+// e(P1_i, Q1[i1_i]) == e(P2_i, Q2[i2_i]) for device-resident inputs; d_p1 / d_p2 == nullptr means
+// the G1 generator for every check.  flags as hbl::pair_verify.
+int run_pairing_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
+                    const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2,
+                    int flags, uint8_t* d_v, uint32_t* d_value = nullptr) {
+  if (n == 0) return HBH_OK;
+  if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
+  const int impl = resolve_impl(e, n);
+  if (impl == HBH_IMPL_PAIR) return launch_pair(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value);
+  if (!d_p1 || !d_p2) {
+    const void* g = nullptr;
+    int rc = g1_repeated(e, s, n, &g);
+    if (rc) return rc;
+    if (!d_p1) d_p1 = g;
+    if (!d_p2) d_p2 = g;
+  }
+  int rc = launch_prepare(e, s, d_q1, nq1, e->coef1, e->inf1, d_q2, nq2, &e->coef2, &e->inf2);
+  if (rc) return rc;
+  return launch_prepared(e, s, impl, n, d_p1, nq1, d_i1, d_p2, nq2, d_i2, flags, d_v, d_value);
 }
 
 int check_idx(const uint32_t* idx, size_t n, size_t table) {
@@ -163,23 +212,26 @@ int check_idx(const uint32_t* idx, size_t n, size_t table) {
   return HBH_OK;
 }
 
-// Host-pointer pairing-eq: stage to device, run, copy verdicts back, synchronise.
+// Host-pointer pairing-eq: stage to device, run, copy verdicts back, synchronise.  p1 / p2 ==
+// nullptr: the G1 generator (nothing is uploaded for it).
 int run_pairing_eq_host(hbh_engine* e, size_t n, const uint8_t* p1, const uint8_t* q1, size_t nq1, const uint32_t* i1,
                         const uint8_t* p2, const uint8_t* q2, size_t nq2, const uint32_t* i2, uint8_t* v) {
   if (n == 0) return HBH_OK;
-  if (!p1 || !q1 || !p2 || !q2 || !v) return fail(HBH_ERR_ARG, "null pointer");
+  if (!q1 || !q2 || !v) return fail(HBH_ERR_ARG, "null pointer");
   int rc = check_idx(i1, n, nq1);
   if (rc) return rc;
   rc = check_idx(i2, n, nq2);
   if (rc) return rc;
   hipStream_t s = e->stream;
-  HBH_CHECK(e->in_p1.ensure(n * HBH_G1_BYTES));
-  HBH_CHECK(e->in_p2.ensure(n * HBH_G1_BYTES));
+  rc = begin_call(e, s);
+  if (rc) return rc;
+  if (p1) HBH_CHECK(e->in_p1.ensure(n * HBH_G1_BYTES));
+  if (p2) HBH_CHECK(e->in_p2.ensure(n * HBH_G1_BYTES));
   HBH_CHECK(e->in_q1.ensure(nq1 * HBH_G2_BYTES));
   HBH_CHECK(e->in_q2.ensure(nq2 * HBH_G2_BYTES));
   HBH_CHECK(e->out_v.ensure(n));
-  HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p1, n * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
-  HBH_CHECK(hipMemcpyAsync(e->in_p2.p, p2, n * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
+  if (p1) HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p1, n * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
+  if (p2) HBH_CHECK(hipMemcpyAsync(e->in_p2.p, p2, n * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_q1.p, q1, nq1 * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_q2.p, q2, nq2 * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
   const uint32_t* d_i1 = nullptr;
@@ -194,28 +246,35 @@ int run_pairing_eq_host(hbh_engine* e, size_t n, const uint8_t* p1, const uint8_
     HBH_CHECK(hipMemcpyAsync(e->in_i2.p, i2, n * 4, hipMemcpyHostToDevice, s));
     d_i2 = (const uint32_t*)e->in_i2.p;
   }
-  rc = run_pairing_eq_dev(e, s, n, e->in_p1.p, e->in_q1.p, nq1, d_i1, e->in_p2.p, e->in_q2.p, nq2, d_i2,
-                          (uint8_t*)e->out_v.p);
+  rc = run_pairing_dev(e, s, n, p1 ? e->in_p1.p : nullptr, e->in_q1.p, nq1, d_i1, p2 ? e->in_p2.p : nullptr,
+                       e->in_q2.p, nq2, d_i2, 1, (uint8_t*)e->out_v.p);
   if (rc) return rc;
   HBH_CHECK(hipMemcpyAsync(v, e->out_v.p, n, hipMemcpyDeviceToHost, s));
+  rc = end_call(e, s);
+  if (rc) return rc;
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
 
 // G1 generator in the ABI format (canonical little-endian x || y).
-const std::vector<uint8_t>& g1_generator_bytes() {
-  static const uint32_t w[24] = {
-      0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu,
-      0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u, 0x46c5e7e1u, 0x0caa2329u, 0xa2888ae4u, 0xd03cc744u,
-      0x2c04b3edu, 0x00db18cbu, 0xd5d00af6u, 0xfcf5e095u, 0x741d8ae4u, 0xa09e30edu, 0xe3aaa0f1u, 0x08b3f481u};
-  static std::vector<uint8_t> g((const uint8_t*)w, (const uint8_t*)w + sizeof(w));
-  return g;
-}
+const uint32_t G1_GEN_WORDS[24] = {
+    0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu,
+    0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u, 0x46c5e7e1u, 0x0caa2329u, 0xa2888ae4u, 0xd03cc744u,
+    0x2c04b3edu, 0x00db18cbu, 0xd5d00af6u, 0xfcf5e095u, 0x741d8ae4u, 0xa09e30edu, 0xe3aaa0f1u, 0x08b3f481u};
 
-std::vector<uint8_t> repeat(const std::vector<uint8_t>& rec, size_t n) {
-  std::vector<uint8_t> out(rec.size() * n);
-  for (size_t i = 0; i < n; i++) std::memcpy(out.data() + i * rec.size(), rec.data(), rec.size());
-  return out;
+int g1_repeated(hbh_engine* e, hipStream_t s, size_t n, const void** out) {
+  if (e->g1rep_n < n) {
+    // grown rarely: the device copy persists for the engine's lifetime
+    const size_t want = n + n / 2 + 64;
+    std::vector<uint32_t> h(want * 24);
+    for (size_t i = 0; i < want; i++) std::memcpy(h.data() + i * 24, G1_GEN_WORDS, sizeof(G1_GEN_WORDS));
+    HBH_CHECK(e->g1rep.ensure(want * HBH_G1_BYTES));
+    HBH_CHECK(hipMemcpyAsync(e->g1rep.p, h.data(), want * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipStreamSynchronize(s));
+    e->g1rep_n = want;
+  }
+  *out = e->g1rep.p;
+  return HBH_OK;
 }
 
 }  // namespace
@@ -246,7 +305,10 @@ int hbh_engine_create(int device, hbh_engine** out) {
   hbh_engine* e = new hbh_engine();
   e->device = device;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
+  if (err == hipSuccess) err = hipEventRecord(e->done, e->stream);
   if (err != hipSuccess) {
+    if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return fail(HBH_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(err));
   }
@@ -257,12 +319,14 @@ int hbh_engine_create(int device, hbh_engine** out) {
 int hbh_engine_destroy(hbh_engine* e) {
   if (!e) return HBH_OK;
   (void)hipSetDevice(e->device);
+  (void)hipEventSynchronize(e->done);
   (void)hipStreamSynchronize(e->stream);
   e->timer.clear();
   for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->lc0, &e->lc1, &e->lc2, &e->lc3,
-                    &e->in_p1, &e->in_q1, &e->in_i1,
-                    &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v, &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x})
+                    &e->g1rep, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v, &e->in_a,
+                    &e->in_b, &e->in_c, &e->in_d, &e->out_x})
     b->release();
+  (void)hipEventDestroy(e->done);
   (void)hipStreamDestroy(e->stream);
   delete e;
   return HBH_OK;
@@ -272,6 +336,7 @@ int hbh_verify_pairing_eq(hbh_engine* e, size_t n, const uint8_t* p1, const uint
                           const uint32_t* i1, const uint8_t* p2, const uint8_t* q2, size_t nq2, const uint32_t* i2,
                           uint8_t* v) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (n && (!p1 || !p2)) return fail(HBH_ERR_ARG, "null pointer");
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   return run_pairing_eq_host(e, n, p1, q1, nq1, i1, p2, q2, nq2, i2, v);
@@ -281,27 +346,32 @@ int hbh_verify_pairing_eq_dev(hbh_engine* e, void* stream, size_t n, const void*
                               const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2,
                               const uint32_t* d_i2, uint8_t* d_v) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
-  if (n && (!d_p1 || !d_q1 || !d_p2 || !d_q2 || !d_v)) return fail(HBH_ERR_ARG, "null pointer");
+  if (n && (!d_q1 || !d_q2 || !d_v)) return fail(HBH_ERR_ARG, "null pointer");
   if ((!d_i1 && nq1 != n) || (!d_i2 && nq2 != n)) return fail(HBH_ERR_ARG, "identity index map requires table size == n");
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  return run_pairing_eq_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, d_v);
+  int rc = begin_call(e, s);
+  if (rc) return rc;
+  rc = run_pairing_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, 1, d_v);
+  if (rc) return rc;
+  return end_call(e, s);
 }
 
 int hbh_verify_sig_shares(hbh_engine* e, size_t n, const uint8_t* pks, const uint8_t* sigs, const uint8_t* hashes,
                           size_t ndocs, const uint32_t* doc_idx, uint8_t* v) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
   if (n == 0) return HBH_OK;
-  std::vector<uint8_t> g1s = repeat(g1_generator_bytes(), n);
+  if (!pks || !sigs) return fail(HBH_ERR_ARG, "null pointer");
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
-  return run_pairing_eq_host(e, n, pks, hashes, ndocs, doc_idx, g1s.data(), sigs, n, nullptr, v);
+  return run_pairing_eq_host(e, n, pks, hashes, ndocs, doc_idx, nullptr, sigs, n, nullptr, v);
 }
 
 int hbh_verify_dec_shares(hbh_engine* e, size_t n, const uint8_t* shares, const uint8_t* pks, const uint8_t* huv,
                           const uint8_t* w, size_t ncts, const uint32_t* ct_idx, uint8_t* v) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (n && (!shares || !pks)) return fail(HBH_ERR_ARG, "null pointer");
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   return run_pairing_eq_host(e, n, shares, huv, ncts, ct_idx, pks, w, ncts, ct_idx, v);
@@ -311,10 +381,10 @@ int hbh_verify_ciphertexts(hbh_engine* e, size_t n, const uint8_t* u, const uint
                            uint8_t* v) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
   if (n == 0) return HBH_OK;
-  std::vector<uint8_t> g1s = repeat(g1_generator_bytes(), n);
+  if (!u) return fail(HBH_ERR_ARG, "null pointer");
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
-  return run_pairing_eq_host(e, n, g1s.data(), w, n, nullptr, u, huv, n, nullptr, v);
+  return run_pairing_eq_host(e, n, nullptr, w, n, nullptr, u, huv, n, nullptr, v);
 }
 
 int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q, uint8_t* out) {
@@ -324,6 +394,8 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  int rc = begin_call(e, s);
+  if (rc) return rc;
   HBH_CHECK(e->in_p1.ensure(n * HBH_G1_BYTES));
   HBH_CHECK(e->in_q1.ensure(n * HBH_G2_BYTES));
   HBH_CHECK(e->out_v.ensure(n * 576));
@@ -331,17 +403,20 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
   HBH_CHECK(hipMemcpyAsync(e->in_q1.p, q, n * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
   HBH_CHECK(e->in_p2.ensure(n * HBH_G1_BYTES));
   HBH_CHECK(hipMemsetAsync(e->in_p2.p, 0, n * HBH_G1_BYTES, s));  // second pair inactive (P2 = O)
-  int rc = launch_prepare(e, s, e->in_q1.p, n, e->coef1, e->inf1, e->in_q1.p, n, &e->coef2, &e->inf2);
-  if (rc) return rc;
-  rc = launch_pairing(e, s, n, e->in_p1.p, n, nullptr, e->in_p2.p, n, nullptr, 2, nullptr, (uint32_t*)e->out_v.p);
+  rc = run_pairing_dev(e, s, n, e->in_p1.p, e->in_q1.p, n, nullptr, e->in_p2.p, e->in_q1.p, n, nullptr, 2, nullptr,
+                       (uint32_t*)e->out_v.p);
   if (rc) return rc;
   HBH_CHECK(hipMemcpyAsync(out, e->out_v.p, n * 576, hipMemcpyDeviceToHost, s));
+  rc = end_call(e, s);
+  if (rc) return rc;
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
-  if (!e || impl < HBH_IMPL_THREAD || impl > HBH_IMPL_AUTO) return fail(HBH_ERR_ARG, "bad argument");
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (impl != HBH_IMPL_LANE_COOP && impl != HBH_IMPL_THREAD_SIGNED && impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO)
+    return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;
   return HBH_OK;
@@ -389,6 +464,10 @@ int run_mul(hbh_engine* e, size_t n, const uint8_t* pts, size_t pt_bytes, const 
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(e->in_a.ensure(n * pt_bytes));
   HBH_CHECK(e->in_b.ensure(n * HBH_FR_BYTES));
   HBH_CHECK(e->out_x.ensure(n * pt_bytes));
@@ -398,6 +477,10 @@ int run_mul(hbh_engine* e, size_t n, const uint8_t* pts, size_t pt_bytes, const 
   HBH_CHECK(launch(s, (int)n, e->in_a.p, (const uint32_t*)e->in_b.p, e->out_x.p));
   e->timer.end(s, t);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * pt_bytes, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
@@ -420,6 +503,10 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
   HBH_CHECK(e->in_b.ensure(ncomb * m * pb));
   HBH_CHECK(e->out_x.ensure(ncomb * pb));
@@ -437,6 +524,10 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * pb, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
@@ -477,16 +568,16 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
     if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
     xs[k] = idx[k] + 1;
   }
-  // P1 = master pk (repeated), P2 = g1 (repeated): one staging buffer, pk records then g1 records
-  std::vector<uint8_t> p12(2 * ncomb * HBH_G1_BYTES);
-  const std::vector<uint8_t>& g1 = g1_generator_bytes();
-  for (size_t c = 0; c < ncomb; c++) {
-    std::memcpy(p12.data() + c * HBH_G1_BYTES, master_pk, HBH_G1_BYTES);
-    std::memcpy(p12.data() + (ncomb + c) * HBH_G1_BYTES, g1.data(), HBH_G1_BYTES);
-  }
+  // P1 = master pk (one record per combine), P2 = the G1 generator (a flag, nothing uploaded)
+  std::vector<uint8_t> p12(ncomb * HBH_G1_BYTES);
+  for (size_t c = 0; c < ncomb; c++) std::memcpy(p12.data() + c * HBH_G1_BYTES, master_pk, HBH_G1_BYTES);
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
   HBH_CHECK(e->in_b.ensure(ncomb * m * HBH_G2_BYTES));
   HBH_CHECK(e->in_q1.ensure(ncomb * HBH_G2_BYTES));
@@ -503,13 +594,16 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
   HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
                             (int*)e->status.p));
   e->timer.end(s, tm);
-  const uint8_t* d_p = (const uint8_t*)e->in_p1.p;
-  rc = run_pairing_eq_dev(e, s, ncomb, d_p, e->in_q1.p, ncomb, nullptr, d_p + ncomb * HBH_G1_BYTES, e->out_x.p, ncomb,
-                          nullptr, (uint8_t*)e->out_v.p);
+  rc = run_pairing_dev(e, s, ncomb, e->in_p1.p, e->in_q1.p, ncomb, nullptr, nullptr, e->out_x.p, ncomb, nullptr, 1,
+                       (uint8_t*)e->out_v.p);
   if (rc) return rc;
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * HBH_G2_BYTES, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, ncomb, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
@@ -527,6 +621,10 @@ int hbh_bivar_row(hbh_engine* e, size_t nrow, int t, size_t nparts, const uint8_
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   const size_t nout = nrow * (t + 1);
   HBH_CHECK(e->in_a.ensure(nparts * ncoef * HBH_G1_BYTES));
   HBH_CHECK(e->in_b.ensure(nrow * 4));
@@ -540,6 +638,10 @@ int hbh_bivar_row(hbh_engine* e, size_t nrow, int t, size_t nparts, const uint8_
                            e->out_x.p));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, nout * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
@@ -589,6 +691,10 @@ int run_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uin
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(e->in_a.ensure(xw.size() * 4));
   HBH_CHECK(e->in_b.ensure(n));
   HBH_CHECK(e->out_x.ensure(n * pb));
@@ -605,6 +711,10 @@ int run_decompress(hbh_engine* e, size_t n, const uint8_t* in, uint8_t* out, uin
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * pb, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipMemcpyAsync(ok, e->out_v.p, n, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
@@ -632,6 +742,10 @@ int hbh_commitment_eval(hbh_engine* e, size_t n, int t, size_t ncommits, const u
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   const size_t cbytes = ncommits * (size_t)(t + 1) * HBH_G1_BYTES;
   HBH_CHECK(e->in_a.ensure(cbytes));
   HBH_CHECK(e->in_b.ensure(n * 4));
@@ -645,6 +759,10 @@ int hbh_commitment_eval(hbh_engine* e, size_t n, int t, size_t ncommits, const u
                              e->out_x.p));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
@@ -681,6 +799,10 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(e->in_a.ensure(nparts * ncoef * HBH_G1_BYTES));
   HBH_CHECK(e->in_b.ensure(nrow * 8 + nack * 8));
   HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
@@ -701,6 +823,10 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, (uint8_t*)e->out_v.p));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, nack, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }

@@ -11,7 +11,8 @@
 // register footprint and run several waves per SIMD; the wave scheduler, not the compiler, hides
 // the MAD latency.  Stages communicate through HBM in a lane-major layout
 // (word w of lane (check, k) at buf[w * lstride + check * 6 + k]: a wave reads 256 contiguous bytes).
-// Same formulas and verdict as k_pairing_eq (kernels.hpp); line tables come from k_g2_prepare.
+// Same formulas and verdict as pairing.hpp (miller loop + final_exp_x3); line tables come from
+// k_g2_prepare.
 #include <hip/hip_runtime.h>
 
 #include "launch.hpp"

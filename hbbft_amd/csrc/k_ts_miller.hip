@@ -1,5 +1,5 @@
 // HBH_IMPL_THREAD_SIGNED, stage 1: the two-pair Miller loop, one thread per check, signed limbs.
-// Same line tables (k_g2_prepare) and the same product as hb::miller_2pairs (kernels.hpp); the
+// Same line tables (k_g2_prepare) and the same product as the pairing.hpp Miller loop; the
 // accumulator is kept reduced (|.| < 2p) between Fp12 operations instead of canonical-ish < 2p
 // unsigned, which removes the conditional subtractions from every Fp addition.
 #define HS_MULFN static __device__ __noinline__
@@ -10,7 +10,7 @@ namespace hbs {
 
 struct SLine { Fp2 c0, c1, c4; };
 
-// line table entry (kernels.hpp store_line layout; values normalised, in [0, 2p))
+// line table entry (lines.hpp store_line layout; values normalised, in [0, 2p))
 __device__ __forceinline__ SLine ts_load_line(const int4* __restrict__ coef, int stride, int step, int pt) {
   int32_t w[84];
 #pragma unroll

@@ -1,6 +1,7 @@
 // Host-side launchers of the HIP kernels.  Each kernel family lives in its own translation unit
-// (k_pairing.hip, k_curve.hip) so the Makefile compiles them in parallel; engine.hip owns the
-// C ABI, device buffers and streams and calls only these functions.
+// (k_prepare.hip, k_pair.hip, k_lc.hip, k_ts_*.hip, k_curve.hip, k_wire.hip) so the Makefile
+// compiles them in parallel; engine.hip owns the C ABI, device buffers and streams and calls only
+// these functions.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -14,19 +15,14 @@ constexpr int LINE_Q4 = 21;  // 16-byte chunks per line (3 Fp2 x 14 limbs)
 inline int pad64(size_t n) { return (int)((n + 63) / 64 * 64); }
 inline size_t line_table_bytes(size_t npts) { return (size_t)MILLER_STEPS * LINE_Q4 * pad64(npts) * 16; }
 
-// --------------------------------------------------------------- pairing (k_pairing.hip)
-// Miller-loop line tables of up to two G2 point sets (ABI G2 words) in one launch.
+// --------------------------------------------------------------- line tables (k_prepare.hip)
+// Miller-loop line tables of up to two G2 point sets (ABI G2 words) in one launch, in the layout of
+// the lane-cooperative and one-thread signed kernels.
 hipError_t g2_prepare(hipStream_t s, int n0, const void* pts0, void* coef0, uint8_t* inf0, int n1, const void* pts1,
                       void* coef1, uint8_t* inf1);
-// verdict[i] = e(P1_i, Q1[idx1_i]) == e(P2_i, Q2[idx2_i]) from prepared line tables.
-hipError_t pairing_eq(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
-                      const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,
-                      const uint32_t* idx2, uint8_t* verdict);
-// out[i] = e(P_i, Q_i)^3 as 144 canonical words (debug / parity).
-hipError_t pairing_value(hipStream_t s, int n, const void* p, const void* coef, const uint8_t* inf, uint32_t* out);
 
 // --------------------------------------------------------------- lane-cooperative pairing (k_lc.hip)
-// The same verdicts as pairing_eq (or, with value_out, e(P1,Q1)^3 e(P2,Q2)^3 words when flags has
+// verdict[i] = e(P1_i, Q1[idx1_i]) == e(P2_i, Q2[idx2_i]) from prepared line tables (or, with value_out, e(P1,Q1)^3 e(P2,Q2)^3 words when flags has
 // bit 2 set and P2 = O), six lanes per check; w0..w3 are scratch of lc_state_words(n) int32 each.
 size_t lc_lstride(int n);
 size_t lc_state_words(int n);
@@ -44,6 +40,26 @@ hipError_t ts_miller(hipStream_t s, int n, const void* p1, const void* coef1, in
                      const uint32_t* idx2, int flags, void* w0);
 hipError_t ts_final_exp(hipStream_t s, int n, void* w0, void* w1, void* w2, void* w3, uint8_t* verdict,
                         uint32_t* value_out);
+
+// --------------------------------------------------------------- lane-pair pairing (k_pair.hip)
+// One side of a pairing-equality check.  TABLE side: `lines`/`qinf` from pair_prep over the nq
+// shared G2 points, `idx` picks the table per check.  WALK side (lines == nullptr): `q` holds G2
+// points walked inside the Miller loop, `idx` picks the point per check (nullptr = identity).
+// p == nullptr means the G1 generator for every check.  Indices >= nq yield verdict 0.
+struct PairSideDesc {
+  const void* p;
+  const void* q;
+  const void* lines;
+  const uint8_t* qinf;
+  const uint32_t* idx;
+  size_t nq;
+};
+size_t pair_table_bytes(size_t nq);
+hipError_t pair_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* qinf);
+// flags: bit 0 negates P2 (pairing equality), bit 1 conjugates f (single pairing value, with
+// value_out: e(P1,Q1)^3 e(P2,Q2)^3 as 144 canonical words per check)
+hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
+                       uint8_t* verdict, uint32_t* value_out);
 
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).

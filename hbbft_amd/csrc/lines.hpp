@@ -1,5 +1,5 @@
 // Miller-loop line tables of G2 points (gfx950): the table layout written by k_g2_prepare
-// (k_prepare.hip) and read by the one-thread pairing kernels (kernels.hpp).
+// (k_prepare.hip) and read by the lane-cooperative and one-thread signed pairing kernels.
 #pragma once
 #include "pairing.hpp"
 #include "points.hpp"

@@ -117,10 +117,12 @@ class Engine:
         return bytes(out)[:n]
 
     def verify_pairing_eq_dev(self, stream, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, d_v):
-        """Device-pointer variant (ints are raw device addresses, e.g. torch ``data_ptr()``)."""
+        """Device-pointer variant (ints are raw device addresses, e.g. torch ``data_ptr()``);
+        d_p1 / d_p2 = None means the G1 generator for every item."""
         vp = ctypes.c_void_p
-        check(self._l.hbh_verify_pairing_eq_dev(self._h, vp(stream) if stream else None, n, vp(d_p1), vp(d_q1), nq1,
-                                                vp(d_i1) if d_i1 else None, vp(d_p2), vp(d_q2), nq2,
+        check(self._l.hbh_verify_pairing_eq_dev(self._h, vp(stream) if stream else None, n,
+                                                vp(d_p1) if d_p1 else None, vp(d_q1), nq1,
+                                                vp(d_i1) if d_i1 else None, vp(d_p2) if d_p2 else None, vp(d_q2), nq2,
                                                 vp(d_i2) if d_i2 else None, vp(d_v)))
 
     # ------------------------------------------------------------ combine / scalar mult / DKG
@@ -252,7 +254,8 @@ class Engine:
         return bytes(out)[:n]
 
     def set_pairing_impl(self, impl):
-        """0 = one thread per check (default), 1 = lane-cooperative (six lanes per check)."""
+        """HBH_IMPL_*: 1 = lane-cooperative (six lanes per check), 2 = one thread per check (signed
+        limbs, stage kernels), 3 = auto (default), 4 = lane pair (two lanes per check, fused)."""
         check(self._l.hbh_engine_set_pairing_impl(self._h, int(impl)))
 
     # ------------------------------------------------------------ profiling

@@ -91,7 +91,12 @@ int hbh_verify_ciphertexts(hbh_engine* eng, size_t n, const uint8_t* u, const ui
                            const uint8_t* huv, uint8_t* verdicts);
 
 /* Device-pointer variant of hbh_verify_pairing_eq (inputs already in HBM).  Asynchronous on
- * `stream` (hipStream_t as void*, NULL = engine stream). */
+ * `stream` (hipStream_t as void*, NULL = engine stream).  d_p1 / d_p2 == NULL means the G1
+ * generator for every item (PublicKeyShare::verify_g2 has P2 = g1, Ciphertext::verify P1 = g1).
+ * Calls on different streams are ordered by the engine (each call waits for the previous call's
+ * device work before reusing the engine's workspaces).  Index arrays live in device memory and are
+ * not inspected on the host: with HBH_IMPL_PAIR an index >= its table size yields verdict 0; the
+ * LANE_COOP / THREAD_SIGNED implementations require in-range indices. */
 int hbh_verify_pairing_eq_dev(hbh_engine* eng, void* stream, size_t n,
                               const void* d_p1, const void* d_q1_table, size_t nq1, const uint32_t* d_q1_idx,
                               const void* d_p2, const void* d_q2_table, size_t nq2, const uint32_t* d_q2_idx,
@@ -168,17 +173,24 @@ int hbh_g1_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out
 int hbh_g2_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok);
 
 /* ---------------------------------------------------------------- implementation selection
- * Three pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks
- * them): HBH_IMPL_THREAD (one thread per check, 14x28-bit unsigned limbs, k_pairing.hip),
- * HBH_IMPL_LANE_COOP (six lanes per check, one Fp2 coefficient of the Fp12 accumulator per lane;
- * lowest latency for small batches) and HBH_IMPL_THREAD_SIGNED (one thread per check on signed
- * limbs, stage kernels k_ts_*.hip; highest throughput).  HBH_IMPL_AUTO (the default) picks
- * LANE_COOP below HBH_AUTO_LANE_COOP_MAX checks per call and THREAD_SIGNED from there on
- * (7 ms vs 27 ms for one check, 47 ms vs 26.5 ms for 65,536). */
+ * Pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks them):
+ *   HBH_IMPL_PAIR (k_pair.hip): TWO lanes per check, each lane holding one component of every Fp2
+ *     value; the Miller loop walks per-check G2 points in registers and reads line tables only for
+ *     G2 points shared through an index map; Miller loop and final exponentiation in one kernel.
+ *     Throughput path.
+ *   HBH_IMPL_LANE_COOP (k_lc.hip): six lanes per check, one Fp2 coefficient of the Fp12
+ *     accumulator per lane; lowest latency for small batches.
+ *   HBH_IMPL_THREAD_SIGNED (k_ts_*.hip): one thread per check, stage kernels (round-1 path, kept
+ *     as a cross-check).
+ *   HBH_IMPL_AUTO (the default): LANE_COOP below HBH_AUTO_LANE_COOP_MAX checks per call, PAIR from
+ *     there on.
+ * HBH_IMPL_THREAD (0, the round-1 unsigned one-thread kernel) is retired: selecting it returns
+ * HBH_ERR_ARG. */
 #define HBH_IMPL_THREAD 0
 #define HBH_IMPL_LANE_COOP 1
 #define HBH_IMPL_THREAD_SIGNED 2
 #define HBH_IMPL_AUTO 3
+#define HBH_IMPL_PAIR 4
 #define HBH_AUTO_LANE_COOP_MAX 16384
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 

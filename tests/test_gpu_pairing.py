@@ -13,9 +13,9 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[1, 2, 0, 3], ids=["lane_coop", "thread_signed", "thread", "auto"])
+@pytest.fixture(params=[1, 2, 4, 3], ids=["lane_coop", "thread_signed", "pair", "auto"])
 def eng(engine, request):
-    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_THREAD, and
+    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_PAIR and
     the default HBH_IMPL_AUTO) must give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine
@@ -93,9 +93,10 @@ def test_empty_batch(eng):
     assert eng.verify_sig_shares(b"", b"", bytes(192), None) == b""
 
 
-def test_lane_coop_matches_thread_random_batch(engine):
-    """A 1,000-check random batch (valid, swapped, infinity, ragged vs the 10-checks-per-wave
-    lane-cooperative layout): all implementations and the C oracle agree on every verdict."""
+def test_implementations_agree_random_batch(engine):
+    """A 1,003-check random batch (valid, swapped, infinity, ragged vs the 10-checks-per-wave
+    lane-cooperative and 128-checks-per-workgroup lane-pair layouts): all implementations and the C
+    oracle agree on every verdict."""
     import random
     from oracle import cbls
     rng = random.Random(7)
@@ -122,7 +123,7 @@ def test_lane_coop_matches_thread_random_batch(engine):
     v1 = engine.verify_sig_shares(P, S, hs, D)
     engine.set_pairing_impl(2)
     v2 = engine.verify_sig_shares(P, S, hs, D)
-    engine.set_pairing_impl(0)
+    engine.set_pairing_impl(4)
     v0 = engine.verify_sig_shares(P, S, hs, D)
     engine.set_pairing_impl(3)
     assert v1 == v0
@@ -152,3 +153,10 @@ def test_verify_signatures_public_key_verify(eng):
     got = eng.verify_signatures([a for a, _, _ in items], [b for _, b, _ in items], [c for _, _, c in items])
     want = [int(cbls.verify_g2(a, b, c)) for a, b, c in items]
     assert list(got) == want == [1, 1, 0, 0, 1]
+
+
+def test_retired_thread_impl_rejected(engine):
+    """HBH_IMPL_THREAD (0) is retired from the product build: selecting it is an argument error."""
+    from hbbft_amd._lib import HbhError
+    with pytest.raises(HbhError):
+        engine.set_pairing_impl(0)
