@@ -37,7 +37,7 @@ constexpr int DPP_ODD = 0xF5;   // quad_perm [1,1,3,3]
 HP_D bool lp_even() { return (threadIdx.x & 1) == 0; }
 template <int CTRL>
 HP_D int32_t dpp(int32_t v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 HP_D Fp dpp_fp(const Fp& a) {

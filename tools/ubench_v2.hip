@@ -26,6 +26,8 @@ using namespace hbs;
   } while (0)
 
 // ---------------------------------------------------------------- 1. raw MAD chains
+// K independent accumulators, each step acc = acc * x + y through v_mad_u64_u32 (inline asm so the
+// compiler cannot fold the chain; the carry-out goes to an SGPR pair the chains do not share).
 template <int K>
 __global__ void __launch_bounds__(256) k_mad(uint64_t* out, int iters) {
   extern __shared__ uint32_t lds[];
@@ -41,7 +43,10 @@ __global__ void __launch_bounds__(256) k_mad(uint64_t* out, int iters) {
 #pragma unroll
     for (int r = 0; r < 16; r++)
 #pragma unroll
-      for (int k = 0; k < K; k++) acc[k] += (uint64_t)x[k] * y;
+      for (int k = 0; k < K; k++) {
+        uint64_t cc;
+        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(cc) : "v"(x[k]), "v"(y));
+      }
   }
   uint64_t s = 0;
 #pragma unroll
@@ -247,7 +252,7 @@ int main() {
   CHK(hipMalloc(&d64, 64));
   CHK(hipMemcpy(din, hin, sizeof(hin), hipMemcpyHostToDevice));
   const int rounds = 4;
-  for (int wps : {1, 2, 4}) {
+  for (int wps : {1, 2, 4, 8}) {
     const double lanes = 256.0 * wps * rounds * 256;
     const int it = 512;
     float ms = run(k_mad<1>, wps, rounds, d64, it);
