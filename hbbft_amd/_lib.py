@@ -43,6 +43,17 @@ SIGNATURES = [
     ("hbh_engine_set_pairing_impl", _I, [_P, _I]),
     ("hbh_engine_set_profiling", _I, [_P, _I]),
     ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),
+    # host stage (no engine, no GPU)
+    ("hbh_host_last_error", _c.c_char_p, []),
+    ("hbh_hash_g2", _I, [_SZ, _P, _P, _P, _I]),
+    ("hbh_hash_g1_g2", _I, [_SZ, _P, _P, _P, _P, _I]),
+    ("hbh_xor_with_hash", _I, [_SZ, _P, _P, _P, _P, _I]),
+    ("hbh_signature_parity", _I, [_SZ, _P, _P]),
+    ("hbh_g1_compress", _I, [_SZ, _P, _P]),
+    ("hbh_g2_compress", _I, [_SZ, _P, _P]),
+    ("hbh_host_g1_mul", _I, [_SZ, _P, _P, _P, _I]),
+    ("hbh_host_g2_mul", _I, [_SZ, _P, _P, _P, _I]),
+    ("hbh_encrypt", _I, [_SZ, _P, _I, _P, _P, _P, _P, _P, _P, _I]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
 IMPL_LANE_COOP, IMPL_THREAD_SIGNED, IMPL_AUTO, IMPL_PAIR = 1, 2, 3, 4   # HBH_IMPL_* (0 = retired THREAD)
@@ -72,6 +83,11 @@ def lib():
 def check(rc):
     if rc != 0:
         raise HbhError("hbbft_hip error %d: %s" % (rc, lib().hbh_last_error().decode()))
+
+
+def check_host(rc):
+    if rc != 0:
+        raise HbhError("hbbft_hip host stage error %d: %s" % (rc, lib().hbh_host_last_error().decode()))
 
 
 def buf(b):

@@ -172,6 +172,41 @@ int hbh_g1_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out
  * out = ABI G2 points.  Same ok / all-zero convention as hbh_g1_decompress. */
 int hbh_g2_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out, uint8_t* ok);
 
+/* ---------------------------------------------------------------- host stage (CPU, no engine)
+ * What the north star keeps on the host, batched over `threads` std::thread workers (0 = all
+ * hardware threads).  Variable-length inputs are concatenated in `data` with n+1 ascending byte
+ * offsets (item i = data[offsets[i] .. offsets[i+1])).  Conventions: host_hash.cpp header and
+ * SURVEY.md Appendix B.  Error text of these functions: hbh_host_last_error().
+ *   hbh_hash_g2       threshold_crypto hash_g2(msg) -> G2 (ThresholdSign::set_document,
+ *                     src/threshold_sign.rs:151; BA coin documents, binary_agreement.rs:442)
+ *   hbh_hash_g1_g2    hash_g1_g2(U, V) -> G2 (Ciphertext::verify / verify_decryption_share's H_uv,
+ *                     src/threshold_decrypt.rs:142,227)
+ *   hbh_xor_with_hash V xor ChaCha20(sha3(compress(g))) low bytes; out has data's layout
+ *                     (PublicKeySet::decrypt, src/threshold_decrypt.rs:249; SecretKey::decrypt,
+ *                     src/sync_key_gen.rs:505,537)
+ *   hbh_signature_parity  Signature::parity() per G2 point (the BA coin, binary_agreement.rs:402)
+ *   hbh_g1_compress / hbh_g2_compress  pairing 0.14 compressed encodings (48 / 96 B)
+ *   hbh_host_g1_mul / hbh_host_g2_mul  k * P with SECRET k on the host: SecretKeyShare::sign_g2
+ *                     (threshold_sign.rs:167), decrypt_share_no_verify (threshold_decrypt.rs:161),
+ *                     SecretKey::decrypt's U * sk (sync_key_gen.rs:505,537)
+ *   hbh_encrypt       PublicKey::encrypt_with_rng with caller-drawn Fr nonces (32 B LE each):
+ *                     U = g1 r, V = msg xor stream(pk r), W = hash_g1_g2(U, V) r
+ *                     (sync_key_gen.rs:346-357,386-390; honey_badger/epoch_state.rs:224-237);
+ *                     pks holds one key, or one per item when pk_per_item != 0 */
+const char* hbh_host_last_error(void);
+int hbh_hash_g2(size_t n, const uint8_t* data, const size_t* offsets, uint8_t* out, int threads);
+int hbh_hash_g1_g2(size_t n, const uint8_t* u, const uint8_t* data, const size_t* offsets, uint8_t* out,
+                   int threads);
+int hbh_xor_with_hash(size_t n, const uint8_t* g, const uint8_t* data, const size_t* offsets, uint8_t* out,
+                      int threads);
+int hbh_signature_parity(size_t n, const uint8_t* sigs, uint8_t* out);
+int hbh_g1_compress(size_t n, const uint8_t* pts, uint8_t* out);
+int hbh_g2_compress(size_t n, const uint8_t* pts, uint8_t* out);
+int hbh_host_g1_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out, int threads);
+int hbh_host_g2_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out, int threads);
+int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* data, const size_t* offsets,
+                const uint8_t* nonces, uint8_t* u_out, uint8_t* v_out, uint8_t* w_out, int threads);
+
 /* ---------------------------------------------------------------- implementation selection
  * Pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks them):
  *   HBH_IMPL_PAIR (k_pair.hip): TWO lanes per check, each lane holding one component of every Fp2
