@@ -53,6 +53,7 @@ SIGNATURES = [
     ("hbh_g2_compress", _I, [_SZ, _P, _P]),
     ("hbh_host_g1_mul", _I, [_SZ, _P, _P, _P, _I]),
     ("hbh_host_g2_mul", _I, [_SZ, _P, _P, _P, _I]),
+    ("hbh_host_g1_add", _I, [_SZ, _P, _P, _P]),
     ("hbh_encrypt", _I, [_SZ, _P, _I, _P, _P, _P, _P, _P, _P, _I]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2

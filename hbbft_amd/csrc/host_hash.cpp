@@ -454,6 +454,18 @@ int hbh_host_g2_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_
   return bad ? host_fail(HBH_ERR_ARG, "coordinate >= p") : HBH_OK;
 }
 
+int hbh_host_g1_add(size_t n, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  if (n == 0) return HBH_OK;
+  if (!a || !b || !out) return host_fail(HBH_ERR_ARG, "null pointer");
+  for (size_t i = 0; i < n; i++) {
+    hh::Jac<hh::Fq> p, q;
+    if (!hh::g1_from_abi(a + i * HBH_G1_BYTES, p) || !hh::g1_from_abi(b + i * HBH_G1_BYTES, q))
+      return host_fail(HBH_ERR_ARG, "coordinate >= p");
+    hh::g1_to_abi(hh::jac_add(p, q), out + i * HBH_G1_BYTES);
+  }
+  return HBH_OK;
+}
+
 int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* data, const size_t* offsets,
                 const uint8_t* nonces, uint8_t* u_out, uint8_t* v_out, uint8_t* w_out, int threads) {
   if (n == 0) return HBH_OK;

@@ -121,6 +121,19 @@ def g2_mul(pts, scalars, threads=0):
     return _mul(_lib.lib().hbh_host_g2_mul, G2_BYTES, pts, scalars, threads)
 
 
+def g1_add(a, b):
+    """a[i] + b[i] for public G1 points."""
+    l = _lib.lib()
+    n = len(a)
+    if len(b) != n:
+        raise ValueError("length mismatch")
+    ka, pa = _buf(b"".join(bytes(x) for x in a))
+    kb, pb = _buf(b"".join(bytes(x) for x in b))
+    o, po = _out(n * G1_BYTES)
+    check_host(l.hbh_host_g1_add(n, pa, pb, po))
+    return _split(bytes(o), G1_BYTES, n)
+
+
 def encrypt(pks, msgs, nonces, threads=0):
     """PublicKey::encrypt_with_rng per message with caller-drawn nonces: [(U, V, W)].  pks: one
     key for all messages, or one per message."""

@@ -189,6 +189,8 @@ int hbh_g2_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out
  *   hbh_host_g1_mul / hbh_host_g2_mul  k * P with SECRET k on the host: SecretKeyShare::sign_g2
  *                     (threshold_sign.rs:167), decrypt_share_no_verify (threshold_decrypt.rs:161),
  *                     SecretKey::decrypt's U * sk (sync_key_gen.rs:505,537)
+ *   hbh_host_g1_add   out[i] = a[i] + b[i] (public points; SyncKeyGen::generate's sum of
+ *                     commitment rows, src/sync_key_gen.rs:449)
  *   hbh_encrypt       PublicKey::encrypt_with_rng with caller-drawn Fr nonces (32 B LE each):
  *                     U = g1 r, V = msg xor stream(pk r), W = hash_g1_g2(U, V) r
  *                     (sync_key_gen.rs:346-357,386-390; honey_badger/epoch_state.rs:224-237);
@@ -204,6 +206,7 @@ int hbh_g1_compress(size_t n, const uint8_t* pts, uint8_t* out);
 int hbh_g2_compress(size_t n, const uint8_t* pts, uint8_t* out);
 int hbh_host_g1_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out, int threads);
 int hbh_host_g2_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out, int threads);
+int hbh_host_g1_add(size_t n, const uint8_t* a, const uint8_t* b, uint8_t* out);
 int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* data, const size_t* offsets,
                 const uint8_t* nonces, uint8_t* u_out, uint8_t* v_out, uint8_t* w_out, int threads);
 

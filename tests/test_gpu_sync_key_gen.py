@@ -1,0 +1,106 @@
+"""SyncKeyGen flow through the GPU engine, ported from the reference's tests/sync_key_gen.rs:10-103:
+node counts {1, 2, 3, 4, 8, 15} with threshold max_faulty(n); only the first t+1 Parts are
+handled; Acks come from 2t+1 nodes; not ready before / ready after; every node generates the same
+PublicKeySet; every secret share signs a message whose share verifies against
+public_key_share(idx); the combination of t+1 shares verifies against the master key.  Plus the
+fault paths of handle_part_or_fault / handle_ack_or_fault (sync_key_gen.rs:481-547)."""
+import random
+
+import pytest
+
+from hbbft_amd import hoststage
+from hbbft_amd.sync_key_gen import G1_GEN, R_ORDER, Ack, Ciphertext, Part, SyncKeyGen
+
+pytestmark = pytest.mark.gpu
+MSG = b"Help I'm trapped in a unit test factory"
+
+
+def make_nodes(engine, n, t, rng):
+    sks = [rng.randrange(1, R_ORDER) for _ in range(n)]
+    pks = hoststage.g1_mul([G1_GEN] * n, sks)
+    pub = {i: pks[i] for i in range(n)}
+    nodes, props = [], []
+    for i in range(n):
+        kg, part = SyncKeyGen.new(i, sks[i], pub, t, engine, rng=rng)
+        nodes.append(kg)
+        props.append(part)
+    return nodes, props
+
+
+def test_generator_constant(engine):
+    from hbbft_amd.engine import g1_abi_from_uncompressed
+    g1_unc = bytes.fromhex(
+        "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
+        "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
+    assert G1_GEN == g1_abi_from_uncompressed(g1_unc)
+
+
+@pytest.mark.parametrize("node_num", [1, 2, 3, 4, 8, 15])
+def test_sync_key_gen(engine, node_num):
+    t = (node_num - 1) // 3  # util::max_faulty
+    rng = random.Random(1000 + node_num)
+    nodes, props = make_nodes(engine, node_num, t, rng)
+    # the first t+1 proposals; Acks of nodes 0..2t are kept, in (proposal, node) order
+    acks = [[] for _ in range(t + 1)]
+    for sender in range(t + 1):
+        for node_id, node in enumerate(nodes):
+            out = node.handle_parts([(sender, props[sender])], rng)[0]
+            assert out.valid and out.ack is not None, out.fault
+            if node_id <= 2 * t:
+                acks[sender].append((node_id, out.ack))
+    # Acks of all proposals but the last: t complete parts, not ready; then the rest: ready
+    first = [a for s in range(t) for a in acks[s]]
+    last = acks[t]
+    for node in nodes:
+        assert not node.is_ready()
+        assert all(o.valid for o in node.handle_acks(first))
+        assert not node.is_ready()
+        assert all(o.valid for o in node.handle_acks(last))
+        assert node.is_ready()
+    pks0, _ = nodes[0].generate()
+    h = hoststage.hash_g2([MSG])[0]
+    sigs = []
+    for idx, node in enumerate(nodes):
+        pks, sk = node.generate()
+        assert sk is not None
+        assert pks == pks0
+        share_pk = pks.public_key_shares(engine, [idx])[0]
+        assert hoststage.g1_mul([G1_GEN], [sk])[0] == share_pk
+        sig = hoststage.g2_mul([h], [sk])[0]
+        assert engine.verify_sig_shares([share_pk], [sig], [h], [0]) == b"\x01"
+        sigs.append(sig)
+    out, st, v = engine.combine_verify_g2(t, [list(range(t + 1))], [sigs[: t + 1]], pks0.public_key(), [h])
+    assert st == [0] and v == b"\x01"
+
+
+def test_sync_key_gen_faults(engine):
+    """PartFault / AckFault paths (sync_key_gen.rs:481-547, 551-588)."""
+    n, t = 4, 1
+    rng = random.Random(77)
+    nodes, props = make_nodes(engine, n, t, rng)
+    node = nodes[1]
+    # RowCount
+    short = Part(props[0].degree, props[0].commit, props[0].rows[:-1])
+    assert node.handle_part(0, short, rng).fault == "RowCount"
+    # valid, then the same Part again (Valid(None)), then a different one (MultipleParts)
+    out = node.handle_part(0, props[0], rng)
+    assert out.valid and out.ack is not None
+    again = node.handle_part(0, props[0], rng)
+    assert again.valid and again.ack is None
+    assert node.handle_part(0, props[2], rng).fault == "MultipleParts"
+    # RowCommitment: sender 2's rows under sender 3's commitment
+    swapped = Part(props[3].degree, props[3].commit, props[2].rows)
+    assert node.handle_part(3, swapped, rng).fault == "RowCommitment"
+    # DecryptRow: a tampered ciphertext for our row fails Ciphertext::verify
+    rows = list(props[2].rows)
+    c = rows[1]
+    rows[1] = Ciphertext(c.u, c.v, props[2].rows[0].w)
+    assert node.handle_part(2, Part(props[2].degree, props[2].commit, rows), rng).fault == "DecryptRow"
+    # Acks: good one from node 0 for part 0; ValueCount; MissingPart; duplicate; ValueCommitment
+    good = nodes[0].handle_part(0, props[0], rng).ack
+    assert node.handle_ack(0, Ack(0, good.values[:-1])).fault == "ValueCount"
+    assert node.handle_ack(0, Ack(1, good.values)).fault == "MissingPart"  # no Part from node 1 handled
+    bad = nodes[2].handle_part(0, props[0], rng).ack  # node 2's values, claimed by node 3
+    outs = node.handle_acks([(0, good), (0, good), (3, bad)])
+    assert outs[0].valid and outs[1].valid and outs[2].fault == "ValueCommitment"
+    assert node.parts[0].acks == {0, 3} and list(node.parts[0].values) == [1]
