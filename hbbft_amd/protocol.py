@@ -9,17 +9,14 @@ or by a driver's pre-verification window in ONE C-ABI call, and combines run thr
 ``hbh_interpolate_g2/g1``.  Verdicts are a pure function of (public key, hash point, share), so
 caching them cannot change which ``Step`` a fault lands in.
 
-What stays on the host, as in the reference and the north star: hashing to G2 (the caller passes
-the document hash point / ``hash_g1_g2(U, V)``), secret-key operations (``sign_g2``,
-``decrypt_share_no_verify``: ``NetworkInfo`` holds callables), and the XOR stream of
-``PublicKeySet::decrypt`` (``xor_with_hash`` below: SHA3-256 + ChaCha20, SURVEY Appendix B.5).
+What stays on the host, as in the reference and the north star: hashing to G2 (``set_document``
+-> ``hash_g2``; ``set_ciphertext`` -> ``hash_g1_g2(U, V)``), secret-key operations (``sign_g2``,
+``decrypt_share_no_verify``: ``NetworkInfo`` holds callables) and the XOR stream of
+``PublicKeySet::decrypt`` -- all through the product host stage (``hbbft_amd.hoststage``, C++).
 """
-import hashlib
-import struct
-
+from . import hoststage
 from ._lib import G1_BYTES, G2_BYTES
 
-P_FIELD = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 
 
 # ------------------------------------------------------------------ Step / faults (src/traits.rs:64-74)
@@ -71,14 +68,18 @@ class ProtocolError(Exception):
 class NetworkInfo:
     """Node ids, the public key set and this node's secret-key operations.
 
-    pk_shares: {node_id: G1 ABI bytes}; master_pk: G1 ABI bytes; t: threshold (num_faulty);
-    sign_g2(H) / decrypt_share(U): this node's secret operations (None for an observer)."""
+    pk_shares: {node_id: G1 ABI bytes}; master_pk: G1 ABI bytes; t: num_faulty (the share-count
+    gate of try_output); threshold: the PublicKeySet's polynomial degree, which sets how many shares
+    are interpolated (combine_signatures / decrypt take threshold + 1; defaults to t as in
+    NetworkInfo::generate_map, src/network_info.rs:174-215); sign_g2(H) / decrypt_share(U): this
+    node's secret operations (None for an observer)."""
 
-    def __init__(self, our_id, node_ids, t, master_pk, pk_shares, sign_g2=None, decrypt_share=None):
+    def __init__(self, our_id, node_ids, t, master_pk, pk_shares, sign_g2=None, decrypt_share=None, threshold=None):
         self.our_id = our_id
         self._ids = sorted(node_ids)
         self._index = {n: i for i, n in enumerate(self._ids)}
         self.t = t
+        self.threshold = t if threshold is None else threshold
         self.master_pk = master_pk
         self.pk_shares = dict(pk_shares)
         self.sign_g2 = sign_g2
@@ -89,6 +90,9 @@ class NetworkInfo:
 
     def num_faulty(self):
         return self.t
+
+    def pk_set_threshold(self):
+        return self.threshold
 
     def public_key_share(self, node_id):
         return self.pk_shares.get(node_id)
@@ -105,9 +109,76 @@ class BatchVerifier:
 
     def __init__(self, engine):
         self.eng = engine
-        self._sig, self._dec = {}, {}
-        self._qsig, self._qdec = [], []
+        self._sig, self._dec, self._ct = {}, {}, {}
+        self._qsig, self._qdec, self._qct = [], [], []
         self.calls = 0
+        self.checks = 0
+        self.max_batch = 0
+        # combines: results by input, and (when recording) the requests a dry run made
+        self._comb_g2, self._comb_g1 = {}, {}
+        self.recording = False
+        self._rec_g2, self._rec_g1 = [], []
+
+    # -------------------------------------------------------------- combines
+    def combine_verify_g2(self, t, idx, shares, master_pk, h):
+        """combine_and_verify_sig's crypto (src/threshold_sign.rs:249-270): (signature, status,
+        verdict) from the cache, or one engine call.  While recording, the request is noted and a
+        valid placeholder is returned (the state machine does not depend on the signature)."""
+        key = (t, tuple(idx), tuple(bytes(s) for s in shares), bytes(master_pk), bytes(h))
+        if key in self._comb_g2:
+            return self._comb_g2.pop(key)  # one combine per instance: consumed on use
+        if self.recording:
+            self._rec_g2.append(key)
+            return bytes(G2_BYTES), 0, True
+        out, st, v = self.eng.combine_verify_g2(t, [list(idx)], [list(shares)], master_pk, [h])
+        self.calls += 1
+        return out[0], st[0], bool(v[0])
+
+    def interpolate_g1(self, t, idx, shares):
+        """PublicKeySet::decrypt's interpolation (src/threshold_decrypt.rs:242-250): (point, status)."""
+        key = (t, tuple(idx), tuple(bytes(s) for s in shares))
+        if key in self._comb_g1:
+            return self._comb_g1.pop(key)
+        if self.recording:
+            self._rec_g1.append(key)
+            return bytes(G1_BYTES), 0
+        out, st = self.eng.interpolate_g1(t, [list(idx)], [list(shares)])
+        self.calls += 1
+        return out[0], st[0]
+
+    def flush_combines(self):
+        """Run every recorded combine in one engine call per kind (t grouped) and cache them."""
+        for t in sorted({k[0] for k in self._rec_g2}):
+            keys = list(dict.fromkeys(k for k in self._rec_g2 if k[0] == t))
+            mpks = {k[3] for k in keys}
+            for mpk in mpks:
+                ks = [k for k in keys if k[3] == mpk]
+                out, st, v = self.eng.combine_verify_g2(t, [list(k[1]) for k in ks], [list(k[2]) for k in ks], mpk,
+                                                        [k[4] for k in ks])
+                self.calls += 1
+                for k, o, s_, vv in zip(ks, out, st, v):
+                    self._comb_g2[k] = (o, s_, bool(vv))
+        for t in sorted({k[0] for k in self._rec_g1}):
+            keys = list(dict.fromkeys(k for k in self._rec_g1 if k[0] == t))
+            out, st = self.eng.interpolate_g1(t, [list(k[1]) for k in keys], [list(k[2]) for k in keys])
+            self.calls += 1
+            for k, o, s_ in zip(keys, out, st):
+                self._comb_g1[k] = (o, s_)
+        self._rec_g2, self._rec_g1 = [], []
+
+    def release_doc(self, h):
+        """Drop the cached verdicts of a terminated ThresholdSign instance (document hash h)."""
+        h = bytes(h)
+        self._sig = {k: v for k, v in self._sig.items() if k[1] != h}
+
+    def release_ct(self, huv, w):
+        """Drop the cached verdicts of a terminated ThresholdDecrypt instance."""
+        key = (bytes(huv), bytes(w))
+        self._dec = {k: v for k, v in self._dec.items() if (k[2], k[3]) != key}
+        self._ct = {k: v for k, v in self._ct.items() if (k[2], k[1]) != key}
+
+    def cached(self):
+        return len(self._sig) + len(self._dec) + len(self._ct) + len(self._comb_g1) + len(self._comb_g2)
 
     # ThresholdSign: PublicKeyShare::verify_g2(share, H)  (src/threshold_sign.rs:223)
     def queue_sig(self, pk, h, share):
@@ -135,7 +206,28 @@ class BatchVerifier:
             self.drain()
         return self._dec[key]
 
+    # Ciphertext::verify  (src/threshold_decrypt.rs:142)
+    def queue_ct(self, ct):
+        key = (bytes(ct.u), bytes(ct.w), bytes(ct.huv))
+        if key not in self._ct:
+            self._qct.append(key)
+
+    def ct_valid(self, ct):
+        key = (bytes(ct.u), bytes(ct.w), bytes(ct.huv))
+        if key not in self._ct:
+            self._qct.append(key)
+            self.drain()
+        return self._ct[key]
+
     def drain(self):
+        if self._qct:
+            keys = list(dict.fromkeys(self._qct))
+            self._qct = []
+            v = self.eng.verify_ciphertexts([k[0] for k in keys], [k[1] for k in keys], [k[2] for k in keys])
+            self.calls += 1
+            self.checks += len(keys)
+            for k, ok in zip(keys, v):
+                self._ct[k] = bool(ok)
         if self._qsig:
             keys = list(dict.fromkeys(self._qsig))
             self._qsig = []
@@ -143,6 +235,8 @@ class BatchVerifier:
             hidx = {h: i for i, h in enumerate(hs)}
             v = self.eng.verify_sig_shares([k[0] for k in keys], [k[2] for k in keys], hs, [hidx[k[1]] for k in keys])
             self.calls += 1
+            self.checks += len(keys)
+            self.max_batch = max(self.max_batch, len(keys))
             for k, ok in zip(keys, v):
                 self._sig[k] = bool(ok)
         if self._qdec:
@@ -153,6 +247,8 @@ class BatchVerifier:
             v = self.eng.verify_dec_shares([k[1] for k in keys], [k[0] for k in keys], [c[0] for c in cts],
                                            [c[1] for c in cts], [cidx[(k[2], k[3])] for k in keys])
             self.calls += 1
+            self.checks += len(keys)
+            self.max_batch = max(self.max_batch, len(keys))
             for k, ok in zip(keys, v):
                 self._dec[k] = bool(ok)
 
@@ -167,8 +263,15 @@ class ThresholdSign:
         self.had_input = False
         self.terminated = False
 
+    def set_document(self, doc):
+        """``set_document`` (:147-153): H = hash_g2(doc) on the host (hbh_hash_g2)."""
+        if self.doc_hash is not None:
+            raise ProtocolError("MultipleMessagesToSign")
+        self.doc_hash = hoststage.hash_g2([bytes(doc)])[0]
+
     def set_document_hash(self, h):
-        """``set_document`` (:147) with ``hash_g2(doc)`` computed by the caller (host hashing)."""
+        """``set_document`` with H already computed, e.g. by a driver that hashes the documents of
+        many instances in one hbh_hash_g2 batch."""
         if self.doc_hash is not None:
             raise ProtocolError("MultipleMessagesToSign")
         self.doc_hash = bytes(h)
@@ -228,71 +331,45 @@ class ThresholdSign:
             sig = self.combine_and_verify_sig()
             self.terminated = True
             step = self.sign()
+            self.verifier.release_doc(self.doc_hash)
             return step.with_output(sig)
         return Step()
 
     def combine_and_verify_sig(self):  # :249-270
-        t = self.netinfo.num_faulty()
+        t = self.netinfo.pk_set_threshold()
         items = [self.received_shares[k] for k in sorted(self.received_shares)][: t + 1]
-        out, st, v = self.verifier.eng.combine_verify_g2(t, [[i for i, _ in items]], [[s for _, s in items]],
-                                                         self.netinfo.master_pk, [self.doc_hash])
-        if st[0] != 0:
+        sig, st, ok = self.verifier.combine_verify_g2(t, [i for i, _ in items], [s for _, s in items],
+                                                      self.netinfo.master_pk, self.doc_hash)
+        if st != 0:
             raise ProtocolError("CombineAndVerifySigCrypto", "DuplicateEntry")
-        if not v[0]:
+        if not ok:
             raise ProtocolError("VerificationFailed")
-        return out[0]
+        return sig
 
 
 # ------------------------------------------------------------------ ThresholdDecrypt (src/threshold_decrypt.rs)
-def _chacha_block(key_words, counter):
-    def rotl(v, c):
-        return ((v << c) & 0xFFFFFFFF) | (v >> (32 - c))
-    s = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574] + list(key_words) + [counter & 0xFFFFFFFF, counter >> 32, 0, 0]
-    x = list(s)
-    for _ in range(10):
-        for a, b, c, d in ((0, 4, 8, 12), (1, 5, 9, 13), (2, 6, 10, 14), (3, 7, 11, 15),
-                           (0, 5, 10, 15), (1, 6, 11, 12), (2, 7, 8, 13), (3, 4, 9, 14)):
-            x[a] = (x[a] + x[b]) & 0xFFFFFFFF
-            x[d] = rotl(x[d] ^ x[a], 16)
-            x[c] = (x[c] + x[d]) & 0xFFFFFFFF
-            x[b] = rotl(x[b] ^ x[c], 12)
-            x[a] = (x[a] + x[b]) & 0xFFFFFFFF
-            x[d] = rotl(x[d] ^ x[a], 8)
-            x[c] = (x[c] + x[d]) & 0xFFFFFFFF
-            x[b] = rotl(x[b] ^ x[c], 7)
-    return [(x[i] + s[i]) & 0xFFFFFFFF for i in range(16)]
-
-
 def g1_compress_abi(p):
-    """ABI G1 bytes -> the 48-byte compressed encoding (zcash flags)."""
-    p = bytes(p)
-    if not any(p):
-        return bytes([0xC0]) + bytes(47)
-    x = int.from_bytes(p[:48], "little")
-    y = int.from_bytes(p[48:], "little")
-    out = bytearray(x.to_bytes(48, "big"))
-    out[0] |= 0x80 | (0x20 if y > (P_FIELD - y) % P_FIELD else 0)
-    return bytes(out)
+    """ABI G1 bytes -> the 48-byte compressed encoding (hbh_g1_compress)."""
+    return hoststage.g1_compress([bytes(p)])[0]
 
 
 def xor_with_hash(g1_abi, data):
-    """threshold_crypto ``xor_with_hash(g, V)``: V xor the low bytes of successive ChaCha20 words
-    keyed by SHA3-256(compress(g)).  Host-side, as in the reference."""
-    key = struct.unpack("<8I", hashlib.sha3_256(g1_compress_abi(g1_abi)).digest())
-    out, block, words, ctr = bytearray(), [], 0, 0
-    for b in bytes(data):
-        if words == len(block):
-            block, words, ctr = _chacha_block(key, ctr), 0, ctr + 1
-        out.append(b ^ (block[words] & 0xFF))
-        words += 1
-    return bytes(out)
+    """threshold_crypto ``xor_with_hash(g, V)`` on the host stage (hbh_xor_with_hash)."""
+    return hoststage.xor_with_hash([bytes(g1_abi)], [bytes(data)])[0]
+
+
+def signature_parity(sig):
+    """``Signature::parity`` -- the coin value of Binary Agreement (binary_agreement.rs:402)."""
+    return hoststage.signature_parity([bytes(sig)])[0]
 
 
 class Ciphertext:
-    """(U in G1, V bytes, W in G2) plus H_uv = hash_g1_g2(U, V), hashed once on the host."""
+    """(U in G1, V bytes, W in G2) plus H_uv = hash_g1_g2(U, V), hashed once on the host (the
+    reference rehashes it in every check; the value is the same)."""
 
-    def __init__(self, u, v, w, huv):
-        self.u, self.v, self.w, self.huv = bytes(u), bytes(v), bytes(w), bytes(huv)
+    def __init__(self, u, v, w, huv=None):
+        self.u, self.v, self.w = bytes(u), bytes(v), bytes(w)
+        self.huv = bytes(huv) if huv is not None else hoststage.hash_g1_g2([self.u], [self.v])[0]
 
 
 class ThresholdDecrypt:
@@ -307,7 +384,7 @@ class ThresholdDecrypt:
     def set_ciphertext(self, ct):  # :138-147
         if self.ciphertext is not None:
             raise ProtocolError("MultipleInputs")
-        if not self.verifier.eng.verify_ciphertexts([ct.u], [ct.w], [ct.huv])[0]:
+        if not self.verifier.ct_valid(ct):
             raise ProtocolError("InvalidCiphertext")
         self.ciphertext = ct
 
@@ -372,13 +449,17 @@ class ThresholdDecrypt:
             return Step()
         self.terminated = True
         step = self.start_decryption()
-        t = self.netinfo.num_faulty()
+        self.verifier.release_ct(self.ciphertext.huv, self.ciphertext.w)
+        t = self.netinfo.pk_set_threshold()
         items = [self.shares[k] for k in sorted(self.shares)][: t + 1]
-        out, st = self.verifier.eng.interpolate_g1(t, [[i for i, _ in items]], [[s for _, s in items]])
-        if st[0] != 0:
+        g, st = self.verifier.interpolate_g1(t, [i for i, _ in items], [s for _, s in items])
+        if st != 0:
             raise ProtocolError("Decryption", "DuplicateEntry")
-        return step.with_output(xor_with_hash(out[0], self.ciphertext.v))
+        if self.verifier.recording:
+            return step.with_output(None)
+        return step.with_output(xor_with_hash(g, self.ciphertext.v))
 
 
 __all__ = ["Fault", "Step", "ProtocolError", "NetworkInfo", "BatchVerifier", "ThresholdSign",
-           "ThresholdDecrypt", "Ciphertext", "xor_with_hash", "g1_compress_abi", "G1_BYTES", "G2_BYTES"]
+           "ThresholdDecrypt", "Ciphertext", "xor_with_hash", "g1_compress_abi", "signature_parity", "G1_BYTES",
+           "G2_BYTES"]

@@ -39,7 +39,7 @@ class Net:
                     self.queue.append((sender, i, payload))
 
 
-def run_sign(engine, n, f, seed, liars=()):
+def run_sign(engine, n, f, seed, liars=(), window=1):
     rng = random.Random(seed)
     coeffs, sks, pks, mpk = keyset(rng, n, f)
     h = cbls.g2_mul(G2, rng.randrange(1, C.R))
@@ -65,13 +65,19 @@ def run_sign(engine, n, f, seed, liars=()):
         faults += [(i, flt) for flt in step.fault_log]
     nodes["observer"].set_document_hash(h)
     while net.queue:
-        sender, target, payload = net.queue.pop(rng.randrange(len(net.queue)))
-        if target in silent or target in liars:
-            continue
-        step = nodes[target].handle_message(sender, payload)
-        net.dispatch(target, step, ids + ["observer"])
-        outputs.setdefault(target, []).extend(step.output)
-        faults += [(target, flt) for flt in step.fault_log]
+        # a window of deliveries: every receiver pre-verifies the shares in it in one drain
+        batch = [net.queue.pop(rng.randrange(len(net.queue))) for _ in range(min(window, len(net.queue)))]
+        batch = [(s_, t_, p_) for s_, t_, p_ in batch if t_ not in silent and t_ not in liars]
+        for sender, target, payload in batch:
+            if nodes[target].doc_hash is not None and sender in pks:
+                nodes[target].verifier.queue_sig(pks[sender], nodes[target].doc_hash, payload)
+        for target in {t_ for _, t_, _ in batch}:
+            nodes[target].verifier.drain()
+        for sender, target, payload in batch:
+            step = nodes[target].handle_message(sender, payload)
+            net.dispatch(target, step, ids + ["observer"])
+            outputs.setdefault(target, []).extend(step.output)
+            faults += [(target, flt) for flt in step.fault_log]
     step = nodes["observer"].handle_input()
     outputs.setdefault("observer", []).extend(step.output)
     return outputs, faults, cbls.g2_mul(h, coeffs[0]), silent, nodes
@@ -89,14 +95,17 @@ def test_threshold_sign_silent_faulty(engine, n, f, seed):
 def test_threshold_sign_lying_nodes_are_blamed(engine):
     n, f = 10, 3
     liars = (8, 9)
-    outputs, faults, want, silent, nodes = run_sign(engine, n, f, 11, liars=liars)
+    outputs, faults, want, silent, nodes = run_sign(engine, n, f, 11, liars=liars, window=24)
     for i in range(n):
         if i not in silent and i not in liars:
             assert outputs[i] == [want]
     assert faults and all(flt.node_id in liars and flt.kind == "UnverifiedSignatureShareSender" for _, flt in faults)
-    # verdicts went through the batched verifier (fewer engine calls than share checks)
-    calls = sum(nodes[i].verifier.calls for i in range(n) if i not in silent and i not in liars)
-    assert calls > 0
+    # verdicts went through the batched verifier (windowed drains): fewer engine calls than checks
+    honest = [i for i in range(n) if i not in silent and i not in liars]
+    calls = sum(nodes[i].verifier.calls for i in honest)
+    checks = sum(nodes[i].verifier.checks for i in honest)
+    assert 0 < calls < checks
+    assert max(nodes[i].verifier.max_batch for i in honest) > 1
 
 
 def test_threshold_sign_errors_and_postponed_verification(engine):
@@ -146,7 +155,8 @@ def test_threshold_decrypt_flow(engine):
     step = nodes[0].handle_input()
     assert [flt.node_id for flt in step.fault_log] == [3]
     assert step.output == [msg]
-    assert nodes[0].verifier.calls == 1
+    # Ciphertext::verify, the three early shares in one drain, the interpolation
+    assert nodes[0].verifier.calls == 3 and nodes[0].verifier.max_batch == 3
     # duplicate share -> MultipleDecryptionShares; invalid ciphertext -> InvalidCiphertext
     nodes[1].set_ciphertext(ct)
     assert nodes[1].handle_message(2, cbls.g1_mul(ct.u, sks[2])).fault_log == []
@@ -157,3 +167,54 @@ def test_threshold_decrypt_flow(engine):
         nodes[2].set_ciphertext(bad)
     assert e.value.kind == "InvalidCiphertext"
     assert xor_with_hash(cbls.g1_mul(G1, 5), b"abc") == tc.xor_with_hash(C.g1_mul(C.G1_GEN, 5), b"abc")
+
+
+def test_threshold_sign_document_and_coin(engine):
+    """set_document(doc) hashes on the host stage (hbh_hash_g2, threshold_sign.rs:147-153); the
+    combined signature is msk * hash_g2(doc) and its parity is the BA coin (binary_agreement.rs:402)."""
+    from hbbft_amd import hoststage
+    from hbbft_amd.protocol import signature_parity
+    rng = random.Random(31)
+    n, f = 4, 1
+    coeffs, sks, pks, mpk = keyset(rng, n, f)
+    doc = (7).to_bytes(8, "little") + (2).to_bytes(8, "little") + (3).to_bytes(4, "little") + (2).to_bytes(8, "little")
+    nodes = {i: ThresholdSign(NetworkInfo(i, range(n), f, mpk, pks,
+                                          sign_g2=lambda H, sk=sks[i]: hoststage.g2_mul([H], [sk])[0]),
+                              BatchVerifier(engine)) for i in range(n)}
+    for node in nodes.values():
+        node.set_document(doc)
+    steps = {i: nodes[i].handle_input() for i in range(n)}
+    shares = {i: steps[i].messages[0][1] for i in range(n)}
+    out = None
+    for j in (1, 2):
+        st = nodes[0].handle_message(j, shares[j])
+        out = st.output or out
+    h = g2a(C.g2_uncompressed(tc.hash_g2(doc)))
+    assert nodes[0].doc_hash == h
+    want = cbls.g2_mul(h, coeffs[0])
+    assert out == [want]
+    assert signature_parity(want) == tc.signature_parity(C.g2_mul(tc.hash_g2(doc), coeffs[0]))
+    assert nodes[0].verifier.cached() == 0  # released at termination
+
+
+def test_threshold_decrypt_raw_ciphertext(engine):
+    """Ciphertexts from encrypt_with_rng on the host stage; H_uv computed by set_ciphertext's
+    Ciphertext (hash_g1_g2 on the host); plaintext recovered byte for byte."""
+    from hbbft_amd import hoststage
+    rng = random.Random(41)
+    n, f = 4, 1
+    coeffs, sks, pks, mpk = keyset(rng, n, f)
+    msg = bytes(rng.randrange(256) for _ in range(90))
+    u, v, w = hoststage.encrypt([mpk], [msg], [rng.randrange(1, C.R)])[0]
+    nodes = {i: ThresholdDecrypt(NetworkInfo(i, range(n), f, mpk, pks,
+                                             decrypt_share=lambda U, sk=sks[i]: hoststage.g1_mul([U], [sk])[0]),
+                                 BatchVerifier(engine)) for i in range(n)}
+    ct = Ciphertext(u, v, w)
+    for node in nodes.values():
+        node.set_ciphertext(ct)
+    steps = {i: nodes[i].handle_input() for i in range(n)}
+    got = None
+    for j in (1, 2):
+        st = nodes[0].handle_message(j, steps[j].messages[0][1])
+        got = st.output or got
+    assert got == [msg]
