@@ -36,8 +36,12 @@ T = F_FAULTY
 NDOCS = 1024
 METRIC = "verified BLS sig shares/sec (whole node) + combine latency, N=64 f=21"
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
-MADS_PER_FPMUL = 2 * 14 * 14          # 14 x 28-bit limbs: product + Montgomery reduction
-PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # v_mad_u64_u32 at half rate: 256 CU x 4 SIMD32 x 2.4 GHz
+# Roofline denominator: measured v_mad_u64_u32 throughput on one MI355X
+# (tools/ubench_v2.hip, profiles/r02/ubench_v2_mad.txt: 8 independent chains per wave), by waves
+# per SIMD; the theoretical half-rate figure is reported beside it.
+MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
+MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
+MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
 IMPLS = {"lane_coop": 1, "thread_signed": 2, "auto": 3, "pair": 4}   # HBH_IMPL_* (include/hbbft_hip.h)
 KERNEL_NAMES = {"lane_coop": "hbs::k_lc_* (miller+easy+exp+glue+verdict)",
                 "thread_signed": "hbs::k_ts_* (miller+easy+exp+glue+verdict)",
@@ -99,21 +103,70 @@ class Workload:
         self.hash_table = b"".join(self.hashes)
 
 
-def cpu_baseline(w, budget_s=12.0):
-    """Reference-equivalent CPU path (oracle/c/bls_cpu.c: pairing 0.14 algorithms, two pairings per
-    check) on a bounded sample of the same workload, one thread and all host threads."""
+def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_simd=None):
+    """One kernel's roofline: achieved = units per launch x algorithmic MADs per unit (workcount,
+    300 per Fp-mul, 222 per Fp-sqr) / average launch time (HIP events on the engine's stream)."""
+    from hbbft_amd import workcount
+    mad = workcount.mads(*op)
+    achieved = units * mad / (avg_ms / 1e3) / 1e12 if avg_ms > 0 else 0.0
+    e = {"kernel": kernel, "launches": launches, "avg_launch_ms": avg_ms, "units_per_launch": units,
+         "unit": unit_name, "fp_ops_per_unit": op[0], "fp_sqr_per_unit": op[1], "mad_per_unit": mad,
+         "achieved": achieved, "peak": MAD_PEAK_MEASURED, "frac": achieved / MAD_PEAK_MEASURED,
+         "peak_theoretical": MAD_PEAK_THEORETICAL}
+    if waves_per_simd:
+        ceil = MAD_CEILING_BY_WAVES.get(waves_per_simd)
+        if ceil is None:  # below one wave per SIMD on average: the 1-wave ceiling scaled by occupancy
+            ceil = MAD_CEILING_BY_WAVES[1] * min(1.0, waves_per_simd)
+        e["waves_per_simd"] = waves_per_simd
+        e["occupancy_ceiling"] = ceil
+        e["frac_of_occupancy_ceiling"] = achieved / ceil
+    return e
+
+
+def pair_waves_per_simd(checks):
+    """k_pair_verify: two lanes per check, 64-lane waves, 1,024 SIMDs."""
+    w = checks * 2 / 64 / 1024
+    return 2 if w >= 2 else (1 if w >= 1 else round(w, 3))
+
+
+def cpu_info():
+    ncpu = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else ncpu
+    # one GPU's share of the host on the GPU pool is 16 threads (box policy); never more than affinity
+    return ncpu, aff, max(1, min(aff, 16))
+
+
+def timed_pool(fn, items, threads):
+    """Run fn over items on `threads` host threads (the C oracle releases the GIL); seconds."""
+    from concurrent.futures import ThreadPoolExecutor
+    t0 = time.perf_counter()
+    if threads == 1:
+        out = [fn(x) for x in items]
+    else:
+        with ThreadPoolExecutor(threads) as ex:
+            out = list(ex.map(fn, items))
+    return time.perf_counter() - t0, out
+
+
+def _ensure_oracle():
     from oracle import cbls
     if not os.path.exists(cbls.LIB_PATH):
         import subprocess
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    return cbls
+
+
+def cpu_baseline(w, budget_s=12.0):
+    """Reference-equivalent CPU path (oracle/c/bls_cpu.c: pairing 0.14 algorithms, two pairings per
+    check) on a bounded sample of the same workload, one thread and all host threads."""
+    cbls = _ensure_oracle()
     n1 = 200
     pk, sg = w.pk_batch[:96 * n1], w.sig_batch[:192 * n1]
     t0 = time.perf_counter()
     v = cbls.verify_g2_batch(pk, sg, w.hash_table, w.doc_idx[:n1], threads=1)
     st = time.perf_counter() - t0
     assert (v == w.expected[:n1]).all(), "CPU baseline verdicts disagree"
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = max(1, min(16, ncpu))
+    ncpu, aff, threads = cpu_info()
     n2 = int(min(len(w.expected), max(threads * 8, (budget_s / (st / n1)) * threads * 0.5)))
     t0 = time.perf_counter()
     v = cbls.verify_g2_batch(w.pk_batch[:96 * n2], w.sig_batch[:192 * n2], w.hash_table, w.doc_idx[:n2],
@@ -131,18 +184,25 @@ def cpu_baseline(w, budget_s=12.0):
     return {"value": n2 / mt, "unit": "shares/s", "cores": threads, "kind": "port",
             "sample": "%d verify_g2 checks of the same batch on %d threads (and %d on 1 thread: %.1f shares/s); "
                       "C restatement of pairing 0.14 (two pairings per check)" % (n2, threads, n1, n1 / st),
-            "single_thread_value": n1 / st, "combine_latency_ms": comb_ms}
+            "single_thread_value": n1 / st, "combine_latency_ms": comb_ms,
+            "nproc": ncpu, "affinity": aff,
+            "all_cores_linear_estimate": n1 / st * ncpu,
+            "cores_note": "measured on the GPU box's CPU share (%d threads); all_cores_linear_estimate = "
+                          "single-thread rate x nproc (%d), an upper bound" % (threads, ncpu)}
 
 
-def pmc_traffic():
-    """HBM bytes per k_pairing_eq launch from the latest committed rocprofv3 --pmc passes
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/<round>/pmc_traffic.json), or None."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the latest committed rocprofv3 --pmc passes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/<round>/pmc_traffic.json), or None
+    when no committed profile covers that kernel."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        with open(fn) as f:
+            d = json.load(f)
+        k = d.get("kernels", {}).get(kernel)
+        if k is not None:
+            return k.get("hbm_bytes_per_launch")
+    return None
 
 
 def combine_latency(eng, w, reps=7):
@@ -220,10 +280,12 @@ def main():
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--impl", choices=["lane_coop", "thread_signed", "pair", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
-    ap.add_argument("--workload", choices=["sign", "decrypt", "dkg"], default="sign",
+    ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
+    ap.add_argument("--workload", choices=["sign", "decrypt", "dkg", "epoch"], default="sign",
                     help="sign = BASELINE configs[1] (default, the headline metric); decrypt = configs[2] "
                          "(64k decryption-share checks + G1 combines, strong-scaled over ranks); dkg = configs[3] "
-                         "(SyncKeyGen N=100 t=33 ack checks of one node)")
+                         "(SyncKeyGen N=100 t=33 ack checks of one node); epoch = configs[4] (HoneyBadger N=100 f=33 "
+                         "epoch crypto of one node)")
     args = ap.parse_args()
     if args.workload != "sign":
         return run_other(args)
@@ -294,8 +356,13 @@ def main():
 
     if rank == 0:
         kern_ms = pair_ms / max(pair_n, 1)
-        fpm = workcount.MILLER_2PAIR + workcount.FINAL_EXP
-        achieved = n * fpm * MADS_PER_FPMUL / (kern_ms / 1e3) / 1e12
+        main_k = roofline_entry(KERNEL_NAMES[args.impl], pair_n, kern_ms, n, workcount.PAIR_CHECK_WALK, "share check",
+                                pair_waves_per_simd(n) if args.impl in ("pair", "auto") else None)
+        kernels = [main_k]
+        if prep_n:
+            kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto") else "hb::k_g2_prepare",
+                                          prep_n, prep_ms / prep_n, nh, workcount.PAIR_PREP_DOC, "document (G2 walk)",
+                                          nh * 2 / 64 / 1024))
         out = {
             "metric": METRIC, "value": value, "unit": "shares/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
@@ -305,12 +372,11 @@ def main():
                        "documents_per_gpu": nh, "n_nodes": N_NODES, "f": F_FAULTY, "pairing_impl": args.impl,
                        "parallelism": "shard-by-batch x%d" % world},
             "verdicts_ok": ok,
-            "roofline": {"bound": "valu",
-                         "kernel": KERNEL_NAMES[args.impl], "achieved": achieved, "peak": PEAK_TMAD,
-                         "unit": "T int32-MAD/s", "frac": achieved / PEAK_TMAD, "traffic": pmc_traffic(),
-                         "kernel_ms": kern_ms, "prepare_ms": prep_ms / max(prep_n, 1),
-                         "work_per_check_fpmul": fpm,
-                         "note": "achieved = checks x (multi-Miller + final-exp Fp-mul) x 392 MAD / kernel time"},
+            "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
+                             traffic=pmc_traffic(KERNEL_NAMES[args.impl]), kernels=kernels,
+                             note="achieved = checks x algorithmic MADs per check (workcount.PAIR_CHECK_WALK: "
+                                  "2-pair Miller + sigma G2 walk + final exp; 300 MAD/Fp-mul, 222/Fp-sqr) / "
+                                  "average launch time; peak = measured MAD rate at 8 waves/SIMD"),
         }
         if not args.no_combine:
             lat, rate, dev_rate = combine_latency(eng, w)
@@ -395,12 +461,17 @@ def run_decrypt(args, eng, world, rank, dev):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    from hbbft_amd._lib import STAGE_PAIRING, STAGE_PREPARE
+    eng.set_profiling(True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(ts)
     for _ in range(args.steps):
         step()
     ev1.record(ts)
     torch.cuda.synchronize(dev)
+    pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
+    prep_ms, prep_n = eng.stage_time(STAGE_PREPARE)
+    eng.set_profiling(False)
     ms_step = _max_over_ranks(ev0.elapsed_time(ev1), world, dev) / args.steps
     # combines: first t+1 valid shares per ciphertext -> g = U * msk
     cidx, cpts = [], []
@@ -408,20 +479,72 @@ def run_decrypt(args, eng, world, rank, dev):
         ids = [k for k in range(N_NODES) if expected[(c - clo) * N_NODES + k]][: T + 1]
         cidx.append(ids)
         cpts.append([shares[(c - clo) * N_NODES + k] for k in ids])
+    from hbbft_amd._lib import STAGE_CURVE
+    from hbbft_amd import workcount
+    eng.interpolate_g1(T, cidx[:8], cpts[:8])  # warm-up
+    eng.set_profiling(True)
     t0 = time.perf_counter()
     out, st = eng.interpolate_g1(T, cidx, cpts)
     comb_s = time.perf_counter() - t0
+    comb_dev_ms, _ = eng.stage_time(STAGE_CURVE)
+    eng.set_profiling(False)
     want = eng.g1_mul(us, [coeffs[0]] * len(mine))
     ok = ok and out == want and all(x == 0 for x in st)
     if rank == 0:
-        print(json.dumps({
+        main_k = roofline_entry("hbs::k_pair_verify<false,false>", pair_n, pair_ms / max(pair_n, 1), n,
+                                workcount.PAIR_CHECK_TABLE, "decryption-share check", pair_waves_per_simd(n))
+        kernels = [main_k]
+        if prep_n:
+            kernels.append(roofline_entry("hbs::k_pair_prep", prep_n, prep_ms / prep_n, 2 * len(mine),
+                                          workcount.PAIR_PREP_DOC, "G2 point (H_uv, W) walk",
+                                          2 * len(mine) * 2 / 64 / 1024))
+        line = {
             "metric": "verified decryption shares/sec (whole node), N=64 f=21", "value": total / (ms_step / 1e3),
             "unit": "shares/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
             "data": "synthetic, seeded (H_uv synthetic in G2; 1/64 invalid shares)",
             "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total,
                        "ciphertexts": ncts, "parallelism": "shard-by-ciphertext x%d" % world},
-            "verdicts_ok": ok, "combines_per_s_rank0": len(mine) / comb_s}), flush=True)
+            "verdicts_ok": ok, "combines_ok": out == want,
+            "combines_per_s_rank0": len(mine) / comb_s,                 # host-to-host, one call
+            "combines_per_s_rank0_device": len(mine) / (comb_dev_ms / 1e3),
+            "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
+                             traffic=pmc_traffic("hbs::k_pair_verify<false,false>"), kernels=kernels,
+                             note="both G2 sides (H_uv, W) are per-ciphertext line tables: per check = 2-pair "
+                                  "Miller + final exp (workcount.PAIR_CHECK_TABLE)"),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_decrypt(shares, pks, huv, ws, us, inst, expected, cidx, cpts,
+                                                        coeffs[0])
+        print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_decrypt(shares, pks, huv, ws, us, inst, expected, cidx, cpts, msk, per_thread=8):
+    """verify_decryption_share (e(D_i, H_uv) == e(pk_i, W), two pairings, C restatement) on a
+    bounded sample, 1 thread and the CPU share; plus one combine_decryption_shares interpolation."""
+    cbls = _ensure_oracle()
+    ncpu, aff, threads = cpu_info()
+    n_nodes = N_NODES
+
+    def check(i):
+        c = int(inst[i])
+        return cbls.pairing_eq(shares[i], huv[c], pks[i % n_nodes], ws[c])
+
+    n1 = 24
+    st, v = timed_pool(check, list(range(n1)), 1)
+    assert v == [bool(x) for x in expected[:n1]], "CPU decrypt verdicts disagree"
+    n2 = threads * per_thread
+    mt, v = timed_pool(check, list(range(n2)), threads)
+    assert v == [bool(x) for x in expected[:n2]], "CPU decrypt verdicts disagree"
+    t0 = time.perf_counter()
+    rc, g = cbls.combine_g1(T, cidx[0], cpts[0])
+    comb_ms = (time.perf_counter() - t0) * 1e3
+    assert rc == 0 and g == cbls.g1_mul(us[0], msk)
+    return {"value": n2 / mt, "unit": "shares/s", "cores": threads, "kind": "port",
+            "sample": "%d decryption-share checks on %d threads (%d on 1 thread: %.1f shares/s); C restatement of "
+                      "pairing 0.14, two pairings per check" % (n2, threads, n1, n1 / st),
+            "single_thread_value": n1 / st, "combine_g1_ms": comb_ms, "nproc": ncpu, "affinity": aff,
+            "all_cores_linear_estimate": n1 / st * ncpu}
 
 
 def run_dkg(args, eng, world, rank, dev):
@@ -465,23 +588,165 @@ def run_dkg(args, eng, world, rank, dev):
     ok = v == expected
     if world > 1:
         dist.barrier()
+    from hbbft_amd._lib import STAGE_CURVE
+    from hbbft_amd import workcount
     times = []
-    for _ in range(max(1, args.steps // 5)):
+    nsteps = max(1, args.steps // 2)
+    eng.set_profiling(True)
+    for _ in range(nsteps):
         t0 = time.perf_counter()
         v = eng.bivar_ack_check(t, parts, pidx, xs, ys, vals)
         times.append((time.perf_counter() - t0) * 1e3)
-    ok = ok and v == expected
-    ms = _max_over_ranks(statistics.median(times), world, dev)
+        ok = ok and v == expected
+    dev_ms, dev_n = eng.stage_time(STAGE_CURVE)
+    eng.set_profiling(False)
+    dev_ms /= max(dev_n, 1)
+    ms = _max_over_ranks(dev_ms, world, dev)
+    host_ms = _max_over_ranks(statistics.median(times), world, dev)
     if rank == 0:
-        print(json.dumps({
-            "metric": "SyncKeyGen ack checks/sec (whole node set), N=100 t=33", "value": len(vals) * world / (ms / 1e3),
-            "unit": "acks/s", "n_gpus": world, "steps": len(times), "warmup": 1, "ms_per_step": ms,
+        nack = len(vals)
+        ops = [workcount.bivar_ack(t, y) for y in ys]
+        op = (sum(o[0] for o in ops) / nack, sum(o[1] for o in ops) / nack)
+        main_k = roofline_entry("hb::k_bivar_row + hb::k_bivar_check", dev_n, dev_ms, nack, op, "ack check",
+                                nack / 64 / 1024)
+        line = {
+            "metric": "SyncKeyGen ack checks/sec (whole node set), N=100 t=33", "value": nack * world / (ms / 1e3),
+            "unit": "acks/s", "n_gpus": world, "steps": nsteps, "warmup": 1, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
             "data": "synthetic, seeded (100 random degree-33 bivariate polynomials; 1/97 tampered values)",
-            "config": {"workload": "SyncKeyGen ack checks of one node, BASELINE configs[3]", "acks_per_rank": len(vals),
+            "config": {"workload": "SyncKeyGen ack checks of one node, BASELINE configs[3]", "acks_per_rank": nack,
                        "parts": n_nodes, "commitment_points": npos, "parallelism": "one node per rank x%d" % world,
-                       "timing": "host-to-host through the C ABI (commitments, values and verdicts cross PCIe)"},
-            "verdicts_ok": ok}), flush=True)
+                       "timing": "device time of the row + check kernels (HIP events); host_to_host_ms includes "
+                                 "the 5.7 MB commitment upload"},
+            "host_to_host_ms": host_ms, "verdicts_ok": ok,
+            "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
+                             traffic=pmc_traffic("hb::k_bivar_check"),
+                             note="one thread per ack, 10,000 acks = 157 waves: latency-bound at this size "
+                                  "(0.15 waves per SIMD)"),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, g1)
+        print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, g1, per_thread=16):
+    """The reference's ack check (BivarCommitment::evaluate(x, y) == g1 * val, sync_key_gen.rs:542,
+    C restatement: 595-term evaluation + one scalar multiplication) on a bounded sample."""
+    cbls = _ensure_oracle()
+    ncpu, aff, threads = cpu_info()
+
+    def check(a):
+        lhs = cbls.bivar_evaluate(t, parts[pidx[a]], xs[a], ys[a])
+        return lhs == cbls.g1_mul(g1, vals[a])
+
+    n1 = 8
+    st, v = timed_pool(check, list(range(n1)), 1)
+    assert v == [bool(expected[a]) for a in range(n1)], "CPU ack verdicts disagree"
+    n2 = threads * per_thread
+    mt, v = timed_pool(check, list(range(n2)), threads)
+    assert v == [bool(expected[a]) for a in range(n2)], "CPU ack verdicts disagree"
+    return {"value": n2 / mt, "unit": "acks/s", "cores": threads, "kind": "port",
+            "sample": "%d ack checks on %d threads (%d on 1 thread: %.1f acks/s); C restatement of "
+                      "BivarCommitment::evaluate + G1 scalar multiplication" % (n2, threads, n1, n1 / st),
+            "single_thread_value": n1 / st, "nproc": ncpu, "affinity": aff,
+            "all_cores_linear_estimate": n1 / st * ncpu}
+
+
+def run_epoch_bench(args, eng, world, rank, dev):
+    """configs[4]: the threshold-crypto work of one node in a HoneyBadger epoch at N=100, f=33
+    (hbbft_amd/honey_badger.py): 100 BA threshold coins + 100 ThresholdDecrypt instances through
+    the mirrored flows with windowed drains and batched combines.  One step = one epoch (a fresh
+    trace each); every rank plays its own node (weak scaling, no collective)."""
+    from hbbft_amd import workcount
+    from hbbft_amd._lib import STAGE_PAIRING
+    from hbbft_amd.honey_badger import EpochTrace, NetworkKeys, run_epoch
+    rng = random.Random(5000 + rank)
+    n, f = 100, 33
+    keys = NetworkKeys(eng, n, f, rng)
+    t0 = time.time()
+    traces = [EpochTrace.generate(eng, keys, rng, hb_epoch=e, proposal_bytes=1000) for e in range(args.warmup + args.steps)]
+    log("generated %d epoch traces in %.1f s" % (len(traces), time.time() - t0))
+    ok = True
+    for tr in traces[:args.warmup]:
+        r = run_epoch(eng, keys, tr, window=args.window)
+        ok = ok and r.plaintexts == tr.proposals
+    if world > 1:
+        dist.barrier()
+    results = []
+    eng.set_profiling(True)
+    t0 = time.perf_counter()
+    for tr in traces[args.warmup:]:
+        results.append(run_epoch(eng, keys, tr, window=args.window))
+    wall = time.perf_counter() - t0
+    pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
+    eng.set_profiling(False)
+    for tr, r in zip(traces[args.warmup:], results):
+        ok = ok and r.plaintexts == tr.proposals and len(r.coins) == len(tr.coin_docs)
+    ms = _max_over_ranks(wall * 1e3 / args.steps, world, dev)
+    if rank == 0:
+        drained = sum(r.checks_gpu for r in results)
+        consumed = sum(r.checks_consumed for r in results) / len(results)
+        phases = {k: sum(r.timing[k] for r in results) / len(results) * 1e3 for k in results[0].timing}
+        main_k = roofline_entry("hbs::k_pair_verify", pair_n, pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
+                                workcount.PAIR_CHECK_WALK, "share / ciphertext check")
+        line = {
+            "metric": "HoneyBadger epochs/sec, one node's threshold crypto, N=100 f=33", "value": world * 1e3 / ms,
+            "unit": "epochs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
+            "data": "synthetic, seeded (dealer key set, 1,000-byte contributions, 100 coin documents per epoch, "
+                    "1/64 forged shares); messages in random order",
+            "config": {"workload": "HoneyBadger epoch crypto trace, BASELINE configs[4]", "n_nodes": n, "f": f,
+                       "coins_per_epoch": len(traces[0].coin_docs), "window": args.window,
+                       "parallelism": "one node per rank x%d" % world,
+                       "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},
+            "outputs_ok": ok, "phase_ms": phases,
+            "engine_calls_per_epoch": sum(r.engine_calls for r in results) / len(results),
+            "checks_drained_per_epoch": drained / len(results), "checks_consumed_per_epoch": consumed,
+            "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)", traffic=None,
+                             note="drains of different sizes (a few thousand checks, 100 ciphertexts, 100 master "
+                                  "verifies) run below one wave per SIMD: latency-bound; no single occupancy ceiling"),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline_epoch(eng, keys, traces[-1], results[-1])
+        print(json.dumps(line), flush=True)
+
+
+def cpu_baseline_epoch(eng, keys, tr, res, sample=12):
+    """The same epoch on the reference-equivalent CPU path: one pairing check (C restatement) per
+    verdict the flows consumed (the reference verifies each share as it arrives, on the node's one
+    thread), one G2 combine + master verify per coin and one G1 interpolation per ciphertext;
+    per-item costs timed on a bounded sample and multiplied by this epoch's counts."""
+    cbls = _ensure_oracle()
+    ncpu, aff, threads = cpu_info()
+    t = keys.t
+    coin = sorted(tr.coin_docs)[0]
+    h = tr.hashes[coin]
+    items = [(j, tr.coin_shares[(coin, j)]) for j in range(1, keys.n)][:sample]
+    t0 = time.perf_counter()
+    for j, sgm in items:
+        cbls.verify_g2(keys.pks[j], sgm, h)
+    per_check = (time.perf_counter() - t0) / len(items)
+    ids = [j for j in range(1, keys.n) if ("coin", coin, j) not in tr.bad][:t + 1]
+    t0 = time.perf_counter()
+    rc, sig = cbls.combine_g2(t, ids, [tr.coin_shares[(coin, j)] for j in ids])
+    ok = cbls.verify_g2(keys.master_pk, sig, h)
+    comb_g2 = time.perf_counter() - t0
+    assert rc == 0 and ok and sig == res.signatures[coin], "CPU coin combine differs"
+    p = 0
+    ids = [j for j in range(1, keys.n) if ("dec", p, j) not in tr.bad][:t + 1]
+    t0 = time.perf_counter()
+    rc, g = cbls.combine_g1(t, ids, [tr.dec_shares[(p, j)] for j in ids])
+    comb_g1 = time.perf_counter() - t0
+    assert rc == 0 and g == cbls.g1_mul(tr.cts[p][0], keys.msk), "CPU decryption combine differs"
+    ncoin, nct = len(res.coins), len(res.plaintexts)
+    epoch_s = res.checks_consumed * per_check + ncoin * comb_g2 + nct * comb_g1
+    return {"value": 1.0 / epoch_s, "unit": "epochs/s", "cores": 1, "kind": "port",
+            "sample": "%d verify_g2 checks, 1 G2 combine+verify, 1 G1 combine timed on one thread, scaled to the "
+                      "epoch's %d consumed checks, %d coins, %d decryptions (a HoneyBadger node handles its "
+                      "messages on one thread)" % (len(items), res.checks_consumed, ncoin, nct),
+            "epoch_ms": epoch_s * 1e3, "per_check_ms": per_check * 1e3, "combine_g2_ms": comb_g2 * 1e3,
+            "combine_g1_ms": comb_g1 * 1e3, "nproc": ncpu, "affinity": aff,
+            "all_cores_linear_estimate": ncpu / epoch_s}
 
 
 def run_other(args):
@@ -491,6 +756,8 @@ def run_other(args):
     eng = Engine(local)
     if args.workload == "decrypt":
         run_decrypt(args, eng, world, rank, dev)
+    elif args.workload == "epoch":
+        run_epoch_bench(args, eng, world, rank, dev)
     else:
         run_dkg(args, eng, world, rank, dev)
     eng.close()

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/hbbft_hip.h"
@@ -779,20 +780,17 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   // one row(x) per distinct (part, x): evaluate(x, y) = sum_j row(x)_j y^j
   std::vector<uint32_t> row_part, row_x, row_of(nack);
   {
-    std::vector<std::pair<uint64_t, uint32_t>> seen;
+    std::unordered_map<uint64_t, uint32_t> seen;
+    seen.reserve(nack < 4096 ? nack : 4096);
     for (size_t a = 0; a < nack; a++) {
       if (part_idx[a] >= nparts) return fail(HBH_ERR_ARG, "part index out of range");
       const uint64_t key = ((uint64_t)part_idx[a] << 32) | xs[a];
-      uint32_t r = 0xffffffffu;
-      for (auto& kv : seen)
-        if (kv.first == key) { r = kv.second; break; }
-      if (r == 0xffffffffu) {
-        r = (uint32_t)row_part.size();
-        seen.push_back({key, r});
+      auto it = seen.emplace(key, (uint32_t)row_part.size());
+      if (it.second) {
         row_part.push_back(part_idx[a]);
         row_x.push_back(xs[a]);
       }
-      row_of[a] = r;
+      row_of[a] = it.first->second;
     }
   }
   const size_t nrow = row_part.size();

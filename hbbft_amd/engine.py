@@ -281,12 +281,36 @@ class Engine:
 
 
 # ------------------------------------------------------------------ wire-format helpers
+P_FIELD = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+
+
+def _check_uncompressed(b, size):
+    """The flag and field checks of pairing 0.14's into_affine_unchecked for the uncompressed
+    encoding: no compression flag (0x80), no sort flag (0x20), an infinity flag (0x40) only with
+    every other bit zero, every coordinate < p.  Returns True for the point at infinity.  (On-curve
+    and subgroup membership are not checked here: the engine's decompress kernels check on-curve,
+    and the subgroup contract is documented in include/hbbft_hip.h.)"""
+    b = bytes(b)
+    if len(b) != size:
+        raise ValueError("uncompressed point must be %d bytes" % size)
+    if b[0] & 0x80:
+        raise ValueError("unexpected compression mode")
+    if b[0] & 0x20:
+        raise ValueError("unexpected information (sort flag)")
+    if b[0] & 0x40:
+        if b[0] != 0x40 or any(b[1:]):
+            raise ValueError("unexpected information (infinity with coordinates)")
+        return True
+    for o in range(0, size, 48):
+        if int.from_bytes(b[o:o + 48], "big") >= P_FIELD:
+            raise ValueError("coordinate not in field")
+    return False
+
+
 def g1_abi_from_uncompressed(b):
     """pairing 0.14 G1Uncompressed (96 B, BE, 0x40 = infinity) -> ABI bytes."""
     b = bytes(b)
-    if len(b) != 96:
-        raise ValueError("G1 uncompressed must be 96 bytes")
-    if b[0] & 0x40:
+    if _check_uncompressed(b, 96):
         return bytes(96)
     return b[0:48][::-1] + b[48:96][::-1]
 
@@ -294,9 +318,7 @@ def g1_abi_from_uncompressed(b):
 def g2_abi_from_uncompressed(b):
     """pairing 0.14 G2Uncompressed (192 B: x.c1 x.c0 y.c1 y.c0, BE) -> ABI (x.c0 x.c1 y.c0 y.c1, LE)."""
     b = bytes(b)
-    if len(b) != 192:
-        raise ValueError("G2 uncompressed must be 192 bytes")
-    if b[0] & 0x40:
+    if _check_uncompressed(b, 192):
         return bytes(192)
     return b[48:96][::-1] + b[0:48][::-1] + b[144:192][::-1] + b[96:144][::-1]
 

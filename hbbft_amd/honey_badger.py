@@ -1,0 +1,240 @@
+"""HoneyBadger epoch crypto trace (BASELINE.json configs[4]).
+
+What one node of a HoneyBadger network does with threshold cryptography in one epoch, replayed
+through the mirrored message flows (hbbft_amd/protocol.py) with windowed BatchVerifier drains:
+
+* Binary Agreement coins (src/binary_agreement/binary_agreement.rs:437-448): a BA instance whose
+  epoch is 2 (mod 3) runs a ThresholdSign on ``bincode((BaSessionId{EpochId{hb_id, epoch},
+  proposer_idx}, ba_epoch))`` (28 bytes, subset.rs:182-185, epoch_state.rs:401-404) and takes the
+  signature's parity as the coin (:395-405).  ``coins`` of the N BA instances reach such an epoch
+  (0 on the all-agree path, where epoch 0's fixed coin decides; N when every instance needs one
+  threshold coin).
+* Threshold decryption (src/honey_badger/epoch_state.rs:376-395): the N accepted contributions are
+  ciphertexts (encrypt_with_rng of the proposer's batch); each goes through set_ciphertext
+  (Ciphertext::verify), our own decryption share and the other nodes' shares, then
+  combine_decryption_shares and the plaintext.
+
+Messages are delivered in seeded random order, ``window`` at a time.  Before a window is delivered
+the node queues the checks its messages will need (for instances that have not terminated) and
+drains them: one engine call per kind per window, instead of one pairing check per message (the
+reference's per-message verify).  Combines are deferred within the epoch and run in one batch
+(BatchVerifier deferred mode); Steps and outputs are identical to per-message processing.
+
+The CPU comparison is the reference-equivalent work: the checks the flows actually consumed
+(``BatchVerifier.lookups``: shares that arrived before their instance terminated) plus the
+combines, timed on the C restatement by bench.py (oracle use stays in bench/tests).
+"""
+import random
+import struct
+import time
+
+from . import hoststage
+from .protocol import BatchVerifier, Ciphertext, Deferred, NetworkInfo, ThresholdDecrypt, ThresholdSign, \
+    signature_parity
+from .sync_key_gen import G1_GEN, R_ORDER
+
+__all__ = ["NetworkKeys", "EpochTrace", "coin_document", "run_epoch", "EpochResult"]
+
+
+def coin_document(hb_id, hb_epoch, proposer_idx, ba_epoch):
+    """bincode of ((BaSessionId{subset_id: EpochId{hb_id, epoch}, proposer_idx}), ba_epoch)."""
+    return struct.pack("<QQIQ", hb_id, hb_epoch, proposer_idx, ba_epoch)
+
+
+def _poly_eval(coeffs, x):
+    r = 0
+    for c in reversed(coeffs):
+        r = (r * x + c) % R_ORDER
+    return r
+
+
+class NetworkKeys:
+    """A synthetic dealer's key set (SecretKeySet::random of degree t): secret shares sk_i =
+    p(i+1), public-key shares g1*sk_i, master key g1*p(0).  Generated with the engine's scalar
+    multiplication (test data, not the measured path)."""
+
+    def __init__(self, engine, n, t, rng):
+        self.n, self.t = n, t
+        self.coeffs = [rng.randrange(1, R_ORDER) for _ in range(t + 1)]
+        self.sks = [_poly_eval(self.coeffs, i + 1) for i in range(n)]
+        pts = engine.g1_mul([G1_GEN] * (n + 1), self.sks + [self.coeffs[0]])
+        self.pks = {i: pts[i] for i in range(n)}
+        self.master_pk = pts[n]
+
+    @property
+    def msk(self):
+        return self.coeffs[0]
+
+
+class EpochTrace:
+    """Every crypto message node ``our`` receives in one HoneyBadger epoch."""
+
+    def __init__(self, keys, hb_epoch, proposals, cts, coin_docs, coin_shares, dec_shares, coin_msgs, dec_msgs):
+        self.keys, self.hb_epoch = keys, hb_epoch
+        self.proposals = proposals      # proposer -> plaintext contribution
+        self.cts = cts                  # proposer -> (u, v, w) (encrypt_with_rng output)
+        self.coin_docs = coin_docs      # proposer -> 28-byte coin document (BA instances with a coin)
+        self.coin_shares = coin_shares  # (proposer, node) -> signature share
+        self.dec_shares = dec_shares    # (proposer, node) -> decryption share
+        self.coin_msgs = coin_msgs      # [(proposer, sender)] in delivery order
+        self.dec_msgs = dec_msgs        # [(proposer, sender)] in delivery order
+        self.bad = set()                # (kind, proposer, sender) of forged shares
+
+    @classmethod
+    def generate(cls, engine, keys, rng, hb_epoch=0, coins=None, proposal_bytes=256, bad_every=64, hb_id=0,
+                 our=0):
+        n = keys.n
+        coins = n if coins is None else coins
+        proposals = {p: bytes(rng.randrange(256) for _ in range(proposal_bytes)) for p in range(n)}
+        enc = hoststage.encrypt([keys.master_pk], [proposals[p] for p in range(n)],
+                                [rng.randrange(1, R_ORDER) for _ in range(n)])
+        cts = {p: enc[p] for p in range(n)}
+        coin_docs = {p: coin_document(hb_id, hb_epoch, p, 2) for p in rng.sample(range(n), coins)}
+        hashes = dict(zip(coin_docs, hoststage.hash_g2([coin_docs[p] for p in coin_docs]))) if coins else {}
+        others = [j for j in range(n) if j != our]
+        bad = set()
+        # decryption shares D_{p,j} = U_p * sk_j (a few forged: U_p * random)
+        keys_d, bases, scal = [], [], []
+        for p in range(n):
+            for j in others:
+                forged = (p * n + j) % bad_every == 1
+                keys_d.append((p, j))
+                bases.append(cts[p][0])
+                scal.append(rng.randrange(1, R_ORDER) if forged else keys.sks[j])
+                if forged:
+                    bad.add(("dec", p, j))
+        dec_shares = dict(zip(keys_d, engine.g1_mul(bases, scal))) if keys_d else {}
+        keys_s, bases, scal = [], [], []
+        for p in coin_docs:
+            for j in others:
+                forged = (p * n + j) % bad_every == 2
+                keys_s.append((p, j))
+                bases.append(hashes[p])
+                scal.append(rng.randrange(1, R_ORDER) if forged else keys.sks[j])
+                if forged:
+                    bad.add(("coin", p, j))
+        coin_shares = dict(zip(keys_s, engine.g2_mul(bases, scal))) if keys_s else {}
+        coin_msgs = list(keys_s)
+        rng.shuffle(coin_msgs)
+        dec_msgs = list(keys_d)
+        rng.shuffle(dec_msgs)
+        tr = cls(keys, hb_epoch, proposals, cts, coin_docs, coin_shares, dec_shares, coin_msgs, dec_msgs)
+        tr.bad = bad
+        tr.hashes = hashes
+        return tr
+
+
+class EpochResult:
+    def __init__(self):
+        self.coins = {}        # proposer -> bool (signature parity)
+        self.signatures = {}   # proposer -> combined signature (ABI G2)
+        self.plaintexts = {}   # proposer -> bytes
+        self.faults = []       # (instance kind, proposer, Fault)
+        self.timing = {}       # phase -> seconds
+        self.engine_calls = 0
+        self.checks_gpu = 0    # checks drained through the engine (incl. post-termination window tail)
+        self.checks_consumed = 0  # verdicts the flows used (the reference's per-message checks)
+        self.combines = 0
+
+
+def _deliver(verifier, msgs, window, instance, queue, handle, res, kind):
+    """Deliver msgs in windows: queue the checks of messages whose instance is still running,
+    drain once, then hand every message to its instance."""
+    for w0 in range(0, len(msgs), window):
+        batch = msgs[w0:w0 + window]
+        for p, j in batch:
+            if not instance[p].terminated:
+                queue(p, j)
+        verifier.drain()
+        for p, j in batch:
+            step = handle(p, j)
+            res.faults += [(kind, p, f) for f in step.fault_log]
+            if step.output:
+                yield p, step.output[0]
+
+
+def run_epoch(engine, keys, trace, window=4096, our=0, threads=0):
+    """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain."""
+    res = EpochResult()
+    ver = BatchVerifier(engine)
+    ver.recording = True                   # combines of the epoch run in one batch at the end
+    sk = keys.sks[our]
+    n = keys.n
+    t_all = time.perf_counter()
+
+    # --- Binary Agreement coins: ThresholdSign per BA instance that reaches a coin epoch
+    t0 = time.perf_counter()
+    ver.hash_docs([trace.coin_docs[p] for p in trace.coin_docs])
+    own_sig = {}
+    ni_sign = NetworkInfo(our, range(n), keys.t, keys.master_pk, keys.pks,
+                          sign_g2=lambda H: own_sig[bytes(H)])
+    ts = {p: ThresholdSign(ni_sign, ver) for p in trace.coin_docs}
+    for p, inst in ts.items():
+        inst.set_document(trace.coin_docs[p])
+    hs = [ts[p].doc_hash for p in ts]
+    for h, s in zip(hs, hoststage.g2_mul(hs, [sk] * len(hs), threads=threads) if hs else []):
+        own_sig[bytes(h)] = s
+        ver.queue_sig(keys.pks[our], h, s)  # sign() handles our own share as a message (:176)
+    res.timing["coin_setup"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    coin_out = {}
+    for p, inst in ts.items():
+        step = inst.handle_input()
+        if step.output:
+            coin_out[p] = step.output[0]
+    for p, out in _deliver(ver, trace.coin_msgs, window, ts,
+                           lambda p, j: ver.queue_sig(keys.pks[j], ts[p].doc_hash, trace.coin_shares[(p, j)]),
+                           lambda p, j: ts[p].handle_message(j, trace.coin_shares[(p, j)]), res, "coin"):
+        coin_out[p] = out
+    res.timing["coin_verify"] = time.perf_counter() - t0
+
+    # --- Subset output: the N ciphertexts into ThresholdDecrypt
+    t0 = time.perf_counter()
+    ps = sorted(trace.cts)
+    huv = hoststage.hash_g1_g2([trace.cts[p][0] for p in ps], [trace.cts[p][1] for p in ps], threads=threads)
+    cts = {p: Ciphertext(trace.cts[p][0], trace.cts[p][1], trace.cts[p][2], h) for p, h in zip(ps, huv)}
+    own_dec = dict(zip(ps, hoststage.g1_mul([cts[p].u for p in ps], [sk] * len(ps), threads=threads)))
+    by_u = {cts[p].u: own_dec[p] for p in ps}
+    ni_dec = NetworkInfo(our, range(n), keys.t, keys.master_pk, keys.pks, decrypt_share=lambda U: by_u[bytes(U)])
+    td = {p: ThresholdDecrypt(ni_dec, ver) for p in ps}
+    for p in ps:
+        ver.queue_ct(cts[p])  # (our own decryption share is not verified, threshold_decrypt.rs:167)
+    ver.drain()
+    res.timing["decrypt_setup"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    dec_out = {}
+    for p in ps:
+        td[p].set_ciphertext(cts[p])
+        step = td[p].handle_input()
+        res.faults += [("dec", p, f) for f in step.fault_log]
+        if step.output:
+            dec_out[p] = step.output[0]
+    for p, out in _deliver(ver, trace.dec_msgs, window, td,
+                           lambda p, j: ver.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], cts[p].huv, cts[p].w),
+                           lambda p, j: td[p].handle_message(j, trace.dec_shares[(p, j)]), res, "dec"):
+        dec_out[p] = out
+    res.timing["decrypt_verify"] = time.perf_counter() - t0
+
+    # --- deferred combines: one G2 combine+verify batch, one G1 interpolation batch
+    t0 = time.perf_counter()
+    ver.flush_combines()
+    res.timing["combine"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    sigs = {}
+    for p, d in coin_out.items():
+        sig, st, ok = d.result if isinstance(d, Deferred) else (d, 0, True)
+        if st != 0 or not ok:
+            raise RuntimeError("coin %d: combined signature does not verify" % p)
+        sigs[p] = sig
+    order = sorted(sigs)
+    res.signatures = sigs
+    res.coins = dict(zip(order, hoststage.signature_parity([sigs[p] for p in order]))) if order else {}
+    order = sorted(dec_out)
+    gs = [dec_out[p].result[0] for p in order]
+    res.plaintexts = dict(zip(order, hoststage.xor_with_hash(gs, [dec_out[p].data for p in order],
+                                                              threads=threads))) if order else {}
+    res.timing["output"] = time.perf_counter() - t0
+    res.timing["epoch"] = time.perf_counter() - t_all
+    res.engine_calls, res.checks_gpu, res.checks_consumed = ver.calls, ver.checks, ver.lookups
+    res.combines = len(coin_out) + len(dec_out)
+    return res

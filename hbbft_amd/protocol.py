@@ -102,6 +102,16 @@ class NetworkInfo:
 
 
 # ------------------------------------------------------------------ verdict cache / batch drain
+class Deferred:
+    """A combine recorded by a BatchVerifier in deferred mode; ``flush_combines`` fills ``result``
+    ((signature, status, verdict) for G2, (point, status) for G1).  ``data`` carries the
+    ciphertext's V for a deferred decryption (the plaintext is xor_with_hash(result[0], data))."""
+    __slots__ = ("key", "result", "data")
+
+    def __init__(self, key, data=None):
+        self.key, self.result, self.data = key, None, data
+
+
 class BatchVerifier:
     """Pure, order-independent verdict cache.  ``queue_*`` records checks; ``drain`` verifies every
     queued check in one engine call per kind; ``*_valid`` returns a cached verdict (or verifies a
@@ -116,8 +126,22 @@ class BatchVerifier:
         self.max_batch = 0
         # combines: results by input, and (when recording) the requests a dry run made
         self._comb_g2, self._comb_g1 = {}, {}
-        self.recording = False
+        self.recording = False  # deferred mode: combines return Deferred, run later in one batch
+        self.lookups = 0        # verdicts the flows consumed (the checks the reference performs)
+        self._docs = {}
         self._rec_g2, self._rec_g1 = [], []
+
+    # -------------------------------------------------------------- host hashing
+    def hash_docs(self, docs):
+        """hash_g2 of many documents in one threaded host-stage call (cached for set_document)."""
+        docs = [bytes(d) for d in docs if bytes(d) not in self._docs]
+        for d, h in zip(docs, hoststage.hash_g2(docs) if docs else []):
+            self._docs[d] = h
+
+    def hash_doc(self, doc):
+        doc = bytes(doc)
+        h = self._docs.pop(doc, None)
+        return h if h is not None else hoststage.hash_g2([doc])[0]
 
     # -------------------------------------------------------------- combines
     def combine_verify_g2(self, t, idx, shares, master_pk, h):
@@ -128,8 +152,9 @@ class BatchVerifier:
         if key in self._comb_g2:
             return self._comb_g2.pop(key)  # one combine per instance: consumed on use
         if self.recording:
-            self._rec_g2.append(key)
-            return bytes(G2_BYTES), 0, True
+            d = Deferred(key)
+            self._rec_g2.append(d)
+            return d, 0, True
         out, st, v = self.eng.combine_verify_g2(t, [list(idx)], [list(shares)], master_pk, [h])
         self.calls += 1
         return out[0], st[0], bool(v[0])
@@ -140,105 +165,112 @@ class BatchVerifier:
         if key in self._comb_g1:
             return self._comb_g1.pop(key)
         if self.recording:
-            self._rec_g1.append(key)
-            return bytes(G1_BYTES), 0
+            d = Deferred(key)
+            self._rec_g1.append(d)
+            return d, 0
         out, st = self.eng.interpolate_g1(t, [list(idx)], [list(shares)])
         self.calls += 1
         return out[0], st[0]
 
     def flush_combines(self):
-        """Run every recorded combine in one engine call per kind (t grouped) and cache them."""
-        for t in sorted({k[0] for k in self._rec_g2}):
-            keys = list(dict.fromkeys(k for k in self._rec_g2 if k[0] == t))
-            mpks = {k[3] for k in keys}
-            for mpk in mpks:
-                ks = [k for k in keys if k[3] == mpk]
-                out, st, v = self.eng.combine_verify_g2(t, [list(k[1]) for k in ks], [list(k[2]) for k in ks], mpk,
-                                                        [k[4] for k in ks])
-                self.calls += 1
-                for k, o, s_, vv in zip(ks, out, st, v):
-                    self._comb_g2[k] = (o, s_, bool(vv))
-        for t in sorted({k[0] for k in self._rec_g1}):
-            keys = list(dict.fromkeys(k for k in self._rec_g1 if k[0] == t))
-            out, st = self.eng.interpolate_g1(t, [list(k[1]) for k in keys], [list(k[2]) for k in keys])
+        """Run every deferred combine: one engine call per (t, master key) for G2 and per t for G1;
+        fills each Deferred's result."""
+        groups = {}
+        for d in self._rec_g2:
+            groups.setdefault((d.key[0], d.key[3]), []).append(d)
+        for (t, mpk), ds in groups.items():
+            out, st, v = self.eng.combine_verify_g2(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds],
+                                                    mpk, [d.key[4] for d in ds])
             self.calls += 1
-            for k, o, s_ in zip(keys, out, st):
-                self._comb_g1[k] = (o, s_)
+            for d, o, s_, vv in zip(ds, out, st, v):
+                d.result = (o, s_, bool(vv))
+        groups = {}
+        for d in self._rec_g1:
+            groups.setdefault(d.key[0], []).append(d)
+        for t, ds in groups.items():
+            out, st = self.eng.interpolate_g1(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds])
+            self.calls += 1
+            for d, o, s_ in zip(ds, out, st):
+                d.result = (o, s_)
         self._rec_g2, self._rec_g1 = [], []
 
     def release_doc(self, h):
         """Drop the cached verdicts of a terminated ThresholdSign instance (document hash h)."""
-        h = bytes(h)
-        self._sig = {k: v for k, v in self._sig.items() if k[1] != h}
+        self._sig.pop(bytes(h), None)
 
     def release_ct(self, huv, w):
         """Drop the cached verdicts of a terminated ThresholdDecrypt instance."""
         key = (bytes(huv), bytes(w))
-        self._dec = {k: v for k, v in self._dec.items() if (k[2], k[3]) != key}
-        self._ct = {k: v for k, v in self._ct.items() if (k[2], k[1]) != key}
+        self._dec.pop(key, None)
+        self._ct.pop(key, None)
 
     def cached(self):
-        return len(self._sig) + len(self._dec) + len(self._ct) + len(self._comb_g1) + len(self._comb_g2)
+        return (sum(len(d) for d in self._sig.values()) + sum(len(d) for d in self._dec.values())
+                + sum(len(d) for d in self._ct.values())
+                + len(self._comb_g1) + len(self._comb_g2))
 
+    # Verdicts are kept per instance (document hash / ciphertext) so that a terminated instance's
+    # entries are released in O(1).
     # ThresholdSign: PublicKeyShare::verify_g2(share, H)  (src/threshold_sign.rs:223)
     def queue_sig(self, pk, h, share):
-        key = (bytes(pk), bytes(h), bytes(share))
-        if key not in self._sig:
-            self._qsig.append(key)
+        h = bytes(h)
+        if (bytes(pk), bytes(share)) not in self._sig.get(h, ()):
+            self._qsig.append((bytes(pk), h, bytes(share)))
 
     def sig_valid(self, pk, h, share):
-        key = (bytes(pk), bytes(h), bytes(share))
-        if key not in self._sig:
-            self._qsig.append(key)
+        self.lookups += 1
+        h, k = bytes(h), (bytes(pk), bytes(share))
+        if k not in self._sig.get(h, ()):
+            self._qsig.append((k[0], h, k[1]))
             self.drain()
-        return self._sig[key]
+        return self._sig[h][k]
 
     # ThresholdDecrypt: PublicKeyShare::verify_decryption_share(share, ct)  (src/threshold_decrypt.rs:227)
     def queue_dec(self, pk, share, huv, w):
-        key = (bytes(pk), bytes(share), bytes(huv), bytes(w))
-        if key not in self._dec:
-            self._qdec.append(key)
+        c = (bytes(huv), bytes(w))
+        if (bytes(pk), bytes(share)) not in self._dec.get(c, ()):
+            self._qdec.append((bytes(pk), bytes(share)) + c)
 
     def dec_valid(self, pk, share, huv, w):
-        key = (bytes(pk), bytes(share), bytes(huv), bytes(w))
-        if key not in self._dec:
-            self._qdec.append(key)
+        self.lookups += 1
+        c, k = (bytes(huv), bytes(w)), (bytes(pk), bytes(share))
+        if k not in self._dec.get(c, ()):
+            self._qdec.append(k + c)
             self.drain()
-        return self._dec[key]
+        return self._dec[c][k]
 
     # Ciphertext::verify  (src/threshold_decrypt.rs:142)
     def queue_ct(self, ct):
-        key = (bytes(ct.u), bytes(ct.w), bytes(ct.huv))
-        if key not in self._ct:
-            self._qct.append(key)
+        c, u = (bytes(ct.huv), bytes(ct.w)), bytes(ct.u)
+        if u not in self._ct.get(c, ()):
+            self._qct.append((u, c[1], c[0]))
 
     def ct_valid(self, ct):
-        key = (bytes(ct.u), bytes(ct.w), bytes(ct.huv))
-        if key not in self._ct:
-            self._qct.append(key)
+        self.lookups += 1
+        c, u = (bytes(ct.huv), bytes(ct.w)), bytes(ct.u)
+        if u not in self._ct.get(c, ()):
+            self._qct.append((u, c[1], c[0]))
             self.drain()
-        return self._ct[key]
+        return self._ct[c][u]
 
     def drain(self):
+        """Verify everything queued: one engine call per kind."""
         if self._qct:
             keys = list(dict.fromkeys(self._qct))
             self._qct = []
             v = self.eng.verify_ciphertexts([k[0] for k in keys], [k[1] for k in keys], [k[2] for k in keys])
-            self.calls += 1
-            self.checks += len(keys)
+            self._count(len(keys))
             for k, ok in zip(keys, v):
-                self._ct[k] = bool(ok)
+                self._ct.setdefault((k[2], k[1]), {})[k[0]] = bool(ok)
         if self._qsig:
             keys = list(dict.fromkeys(self._qsig))
             self._qsig = []
             hs = list(dict.fromkeys(k[1] for k in keys))
             hidx = {h: i for i, h in enumerate(hs)}
             v = self.eng.verify_sig_shares([k[0] for k in keys], [k[2] for k in keys], hs, [hidx[k[1]] for k in keys])
-            self.calls += 1
-            self.checks += len(keys)
-            self.max_batch = max(self.max_batch, len(keys))
+            self._count(len(keys))
             for k, ok in zip(keys, v):
-                self._sig[k] = bool(ok)
+                self._sig.setdefault(k[1], {})[(k[0], k[2])] = bool(ok)
         if self._qdec:
             keys = list(dict.fromkeys(self._qdec))
             self._qdec = []
@@ -246,11 +278,14 @@ class BatchVerifier:
             cidx = {c: i for i, c in enumerate(cts)}
             v = self.eng.verify_dec_shares([k[1] for k in keys], [k[0] for k in keys], [c[0] for c in cts],
                                            [c[1] for c in cts], [cidx[(k[2], k[3])] for k in keys])
-            self.calls += 1
-            self.checks += len(keys)
-            self.max_batch = max(self.max_batch, len(keys))
+            self._count(len(keys))
             for k, ok in zip(keys, v):
-                self._dec[k] = bool(ok)
+                self._dec.setdefault((k[2], k[3]), {})[(k[0], k[1])] = bool(ok)
+
+    def _count(self, n):
+        self.calls += 1
+        self.checks += n
+        self.max_batch = max(self.max_batch, n)
 
 
 # ------------------------------------------------------------------ ThresholdSign (src/threshold_sign.rs)
@@ -267,7 +302,7 @@ class ThresholdSign:
         """``set_document`` (:147-153): H = hash_g2(doc) on the host (hbh_hash_g2)."""
         if self.doc_hash is not None:
             raise ProtocolError("MultipleMessagesToSign")
-        self.doc_hash = hoststage.hash_g2([bytes(doc)])[0]
+        self.doc_hash = self.verifier.hash_doc(doc)
 
     def set_document_hash(self, h):
         """``set_document`` with H already computed, e.g. by a driver that hashes the documents of
@@ -455,8 +490,9 @@ class ThresholdDecrypt:
         g, st = self.verifier.interpolate_g1(t, [i for i, _ in items], [s for _, s in items])
         if st != 0:
             raise ProtocolError("Decryption", "DuplicateEntry")
-        if self.verifier.recording:
-            return step.with_output(None)
+        if isinstance(g, Deferred):
+            g.data = self.ciphertext.v
+            return step.with_output(g)
         return step.with_output(xor_with_hash(g, self.ciphertext.v))
 
 

@@ -1,7 +1,11 @@
-"""Algorithmic work of one share check, in Fp multiplications, derived from the kernel's own
-formulas (csrc/tower.hpp, pairing.hpp, kernels.hpp).  Used by bench.py for the roofline's
-'achieved' figure.  Fp2 mul = 3 Fp-mul (Karatsuba), Fp2 sqr = 2,
-Fp2 x Fp = 2; an Fp squaring counts as one Fp-mul.
+"""Algorithmic work of the hot-path units, in Fp multiplications, derived from the kernels' own
+formulas (csrc/pfp.hpp, k_pair.hip, curve.hpp).  Used by bench.py for the roofline's 'achieved'
+figure.  Fp2 mul = 3 Fp-mul (Karatsuba), Fp2 sqr = 2 (complex), Fp2 x Fp = 2.
+
+Pricing: one Fp multiplication = 300 32x32->64 multiply-adds (12-limb CIOS
+Montgomery: 144 product + 156 reduction); an Fp squaring = 222 (78 product + 144 reduction).
+True Fp squarings occur in the Fp inversion (380 of them) and in the G1 curve formulas
+(dbl-2009-l 2M+5S, madd-2007-bl 7M+4S, add-2007-bl 11M+5S); Fp2/Fp12 squarings are products.
 """
 X_ABS = 0xD201000000010000
 NBITS = X_ABS.bit_length() - 1          # 63 doubling steps
@@ -44,3 +48,46 @@ FP_MULS_PER_CHECK = MILLER_2PAIR + G2_WALK + FINAL_EXP
 if __name__ == "__main__":
     print("miller", MILLER_2PAIR, "g2 walk", G2_WALK, "final exp", FINAL_EXP, "(easy", EASY, "hard", HARD,
           ") total", FP_MULS_PER_CHECK)
+
+
+# ---------------------------------------------------------------------------- MAD pricing
+MAD_PER_FPMUL = 300
+MAD_PER_FPSQR = 222
+FP_INV_SQR = 380                      # square-and-multiply over p-2: 380 squarings
+
+
+def mads(fpmul, fpsqr=0):
+    """32x32->64 multiply-adds of fpmul products (of which fpsqr are squarings)."""
+    return (fpmul - fpsqr) * MAD_PER_FPMUL + fpsqr * MAD_PER_FPSQR
+
+
+# per-unit algorithmic work of each kernel: (Fp ops, of which Fp squarings)
+PAIR_CHECK_WALK = (MILLER_2PAIR + G2_WALK + FINAL_EXP, FP_INV_SQR)   # k_pair_verify, one side walked
+PAIR_CHECK_TABLE = (MILLER_2PAIR + FINAL_EXP, FP_INV_SQR)            # k_pair_verify, both sides tabled
+PAIR_PREP_DOC = (G2_WALK, 0)                                         # k_pair_prep, per G2 point
+
+G1_DBL = (7, 5)
+G1_MADD = (11, 4)
+G1_ADD = (16, 5)
+
+
+def _add(*ops):
+    return (sum(o[0] for o in ops), sum(o[1] for o in ops))
+
+
+def _scale(op, k):
+    return (op[0] * k, op[1] * k)
+
+
+def g1_mul_small(k):
+    """jac_mul_small(P, k): double-and-add from the top bit with full Jacobian additions."""
+    if k <= 1:
+        return (0, 0)
+    return _add(_scale(G1_DBL, k.bit_length() - 1), _scale(G1_ADD, bin(k).count("1") - 1))
+
+
+def bivar_ack(t, y, val_bits=255, val_weight=128):
+    """k_bivar_check for one ack: Horner over the t+1 row points with the small y, then g1 * val
+    (jac_mul_affine: val_bits doublings, val_weight mixed additions) and a cross-multiplied compare."""
+    horner = _scale(_add(g1_mul_small(y), G1_MADD), t + 1)
+    return _add(horner, _scale(G1_DBL, val_bits), _scale(G1_MADD, val_weight), (4, 2))

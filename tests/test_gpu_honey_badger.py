@@ -1,0 +1,66 @@
+"""HoneyBadger epoch crypto trace (BASELINE configs[4]) through the mirrored flows on the GPU
+engine: every decrypted contribution equals the proposal byte for byte, every coin signature is
+msk * hash_g2(coin document) (C oracle) with the oracle's parity, only forged shares are blamed,
+and the windowed drains give the same result as per-message verification (window = 1).
+References: examples/simulation.rs:164-177, 296-316; src/honey_badger/epoch_state.rs:376-395;
+src/binary_agreement/binary_agreement.rs:245-264, 395-405, 437-448."""
+import random
+
+import pytest
+
+from oracle import cbls, tc
+from hbbft_amd.honey_badger import EpochTrace, NetworkKeys, coin_document, run_epoch
+
+pytestmark = pytest.mark.gpu
+
+
+def parity_oracle(sig):
+    x0, x1, y0, y1 = (int.from_bytes(sig[o:o + 48], "little") for o in (0, 48, 96, 144))
+    return tc.signature_parity(((x0, x1), (y0, y1)))
+
+
+def check(trace, res, keys):
+    assert res.plaintexts == trace.proposals
+    assert sorted(res.coins) == sorted(trace.coin_docs)
+    for p, sig in res.signatures.items():
+        assert sig == cbls.g2_mul(trace.hashes[p], keys.msk)
+        assert res.coins[p] == parity_oracle(sig)
+    for kind, p, flt in res.faults:
+        assert (kind, p, flt.node_id) in trace.bad
+        assert flt.kind == ("UnverifiedSignatureShareSender" if kind == "coin" else "UnverifiedDecryptionShareSender")
+
+
+def test_coin_document_layout():
+    d = coin_document(7, 3, 2, 5)
+    assert len(d) == 28 and d[:8] == (7).to_bytes(8, "little") and d[16:20] == (2).to_bytes(4, "little")
+
+
+@pytest.mark.parametrize("n", [4, 7])
+def test_epoch_small_and_window_equivalence(engine, n):
+    t = (n - 1) // 3
+    rng = random.Random(300 + n)
+    keys = NetworkKeys(engine, n, t, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=1, bad_every=5, proposal_bytes=100)
+    big = run_epoch(engine, keys, trace, window=1 << 20)
+    check(trace, big, keys)
+    one = run_epoch(engine, keys, trace, window=1)
+    check(trace, one, keys)
+    assert (one.plaintexts, one.coins, one.signatures) == (big.plaintexts, big.coins, big.signatures)
+    assert [(k, p, f.node_id, f.kind) for k, p, f in one.faults] == [(k, p, f.node_id, f.kind) for k, p, f in big.faults]
+    # per-message verification checks exactly what the flows consume; the big window batches
+    assert one.checks_gpu == one.checks_consumed
+    assert big.engine_calls < one.engine_calls
+
+
+def test_epoch_n100_f33(engine):
+    """configs[4] at full size: N=100, f=33, every BA instance flips one threshold coin."""
+    rng = random.Random(100)
+    keys = NetworkKeys(engine, 100, 33, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=0, proposal_bytes=1000)
+    res = run_epoch(engine, keys, trace, window=4096)
+    check(trace, res, keys)
+    assert len(res.plaintexts) == 100 and len(res.coins) == 100
+    assert res.engine_calls <= 16
+    print("epoch N=100: %.3f s, %d engine calls, %d checks drained, %d consumed, timing %s" % (
+        res.timing["epoch"], res.engine_calls, res.checks_gpu, res.checks_consumed,
+        {k: round(v, 4) for k, v in res.timing.items()}))

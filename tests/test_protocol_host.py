@@ -22,3 +22,21 @@ def test_step_join():
     a.join(b)
     assert a.output == ["sig"] and a.messages == [("all", b"x")]
     assert a.fault_log == [Fault(3, "UnverifiedSignatureShareSender")]
+
+
+def test_uncompressed_flag_and_field_checks():
+    """g1/g2_abi_from_uncompressed reject what pairing 0.14's into_affine_unchecked rejects."""
+    import pytest
+    from hbbft_amd.engine import P_FIELD, g1_abi_from_uncompressed, g2_abi_from_uncompressed
+    from oracle import bls12_381 as C
+    g1 = C.g1_uncompressed(C.G1_GEN)
+    g2 = C.g2_uncompressed(C.G2_GEN)
+    assert g1_abi_from_uncompressed(g1)[:48] == C.G1_GEN[0].to_bytes(48, "little")
+    assert g1_abi_from_uncompressed(bytes([0x40]) + bytes(95)) == bytes(96)
+    assert g2_abi_from_uncompressed(bytes([0x40]) + bytes(191)) == bytes(192)
+    for bad in (bytes([g1[0] | 0x80]) + g1[1:], bytes([g1[0] | 0x20]) + g1[1:], bytes([0x40]) + bytes(94) + b"\x01",
+                P_FIELD.to_bytes(48, "big") + g1[48:], b"\x00" * 95):
+        with pytest.raises(ValueError):
+            g1_abi_from_uncompressed(bad)
+    with pytest.raises(ValueError):
+        g2_abi_from_uncompressed(g2[:96] + P_FIELD.to_bytes(48, "big") + g2[144:])
