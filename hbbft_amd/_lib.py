@@ -43,6 +43,23 @@ SIGNATURES = [
     ("hbh_engine_set_pairing_impl", _I, [_P, _I]),
     ("hbh_engine_set_profiling", _I, [_P, _I]),
     ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),
+    # device-resident variants
+    ("hbh_interpolate_g1_dev", _I, [_P, _P, _SZ, _I, _P, _P, _P, _P]),
+    ("hbh_interpolate_g2_dev", _I, [_P, _P, _SZ, _I, _P, _P, _P, _P]),
+    ("hbh_g1_decompress_dev", _I, [_P, _P, _SZ, _P, _P, _P]),
+    ("hbh_g2_decompress_dev", _I, [_P, _P, _SZ, _P, _P, _P]),
+    ("hbh_bivar_ack_check_dev", _I, [_P, _P, _SZ, _I, _P, _SZ, _P, _P, _P, _P, _P, _P]),
+    # engine pool (multi-device fan-out)
+    ("hbh_pool_create", _I, [_P, _I, _c.POINTER(_P)]),
+    ("hbh_pool_destroy", _I, [_P]),
+    ("hbh_pool_shards", _I, [_P, _c.POINTER(_I)]),
+    ("hbh_pool_engine", _I, [_P, _I, _c.POINTER(_P)]),
+    ("hbh_pool_set_pairing_impl", _I, [_P, _I]),
+    ("hbh_pool_verify_sig_shares", _I, [_P, _SZ, _P, _P, _P, _SZ, _P, _P]),
+    ("hbh_pool_verify_dec_shares", _I, [_P, _SZ, _P, _P, _P, _P, _SZ, _P, _P]),
+    ("hbh_pool_combine_verify_g2", _I, [_P, _SZ, _I, _P, _P, _P, _P, _P, _P, _P]),
+    ("hbh_pool_interpolate_g1", _I, [_P, _SZ, _I, _P, _P, _P, _P]),
+    ("hbh_pool_bivar_ack_check", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P, _P, _P]),
     # host stage (no engine, no GPU)
     ("hbh_host_last_error", _c.c_char_p, []),
     ("hbh_hash_g2", _I, [_SZ, _P, _P, _P, _I]),

@@ -284,6 +284,9 @@ extern "C" {
 
 const char* hbh_last_error(void) { return g_last_error.c_str(); }
 
+// Not part of the public ABI: lets pool.cpp report a shard's failure on the calling thread.
+extern "C" void hbh__set_error(const char* msg) { g_last_error = msg ? msg : ""; }
+
 int hbh_device_count(int* out) {
   if (!out) return fail(HBH_ERR_ARG, "null pointer");
   int c = 0;
@@ -827,6 +830,104 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   }
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- device-resident variants
+// Inputs and outputs in device memory, asynchronous on `stream` (NULL = engine stream), ordered
+// after the engine's previous call like hbh_verify_pairing_eq_dev.
+namespace {
+hipStream_t dev_stream(hbh_engine* e, void* stream) { return stream ? (hipStream_t)stream : e->stream; }
+
+int run_interp_dev(hbh_engine* e, void* stream, size_t ncomb, int t, const uint32_t* d_idx, const void* d_pts,
+                   void* d_out, int* d_status, bool g2) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (ncomb == 0) return HBH_OK;
+  if (!d_idx || !d_pts || !d_out || !d_status) return fail(HBH_ERR_ARG, "null pointer");
+  const size_t m = (size_t)t + 1;
+  if (ncomb * m > (size_t)1 << 26) return fail(HBH_ERR_ARG, "batch too large");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = dev_stream(e, stream);
+  rc = begin_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
+  HBH_CHECK(hipMemsetAsync(d_status, 0, ncomb * sizeof(int), s));
+  HBH_CHECK(hbl::index_plus_one(s, (int)(ncomb * m), (int)m, d_idx, (uint32_t*)e->in_a.p, d_status));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  if (g2)
+    HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status));
+  else
+    HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status));
+  e->timer.end(s, tm);
+  return end_call(e, s);
+}
+
+int run_decompress_dev(hbh_engine* e, void* stream, size_t n, const uint8_t* d_in, void* d_out, uint8_t* d_ok,
+                       bool g2) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (n == 0) return HBH_OK;
+  if (!d_in || !d_out || !d_ok) return fail(HBH_ERR_ARG, "null pointer");
+  if (n > (size_t)1 << 28) return fail(HBH_ERR_ARG, "batch too large");
+  const int nfe = g2 ? 2 : 1;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = dev_stream(e, stream);
+  int rc = begin_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(e->in_a.ensure(n * 12 * nfe * 4));
+  HBH_CHECK(e->in_b.ensure(n));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::wire_parse(s, (int)n, nfe, d_in, (uint32_t*)e->in_a.p, (uint8_t*)e->in_b.p));
+  if (g2)
+    HBH_CHECK(hbl::g2_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, d_out, d_ok));
+  else
+    HBH_CHECK(hbl::g1_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, d_out, d_ok));
+  e->timer.end(s, tm);
+  return end_call(e, s);
+}
+}  // namespace
+
+extern "C" {
+
+int hbh_interpolate_g1_dev(hbh_engine* e, void* stream, size_t ncomb, int t, const uint32_t* d_idx, const void* d_pts,
+                           void* d_out, int* d_status) {
+  return run_interp_dev(e, stream, ncomb, t, d_idx, d_pts, d_out, d_status, false);
+}
+int hbh_interpolate_g2_dev(hbh_engine* e, void* stream, size_t ncomb, int t, const uint32_t* d_idx, const void* d_pts,
+                           void* d_out, int* d_status) {
+  return run_interp_dev(e, stream, ncomb, t, d_idx, d_pts, d_out, d_status, true);
+}
+int hbh_g1_decompress_dev(hbh_engine* e, void* stream, size_t n, const uint8_t* d_in, void* d_out, uint8_t* d_ok) {
+  return run_decompress_dev(e, stream, n, d_in, d_out, d_ok, false);
+}
+int hbh_g2_decompress_dev(hbh_engine* e, void* stream, size_t n, const uint8_t* d_in, void* d_out, uint8_t* d_ok) {
+  return run_decompress_dev(e, stream, n, d_in, d_out, d_ok, true);
+}
+
+int hbh_bivar_ack_check_dev(hbh_engine* e, void* stream, size_t nack, int t, const void* d_commits, size_t nrow,
+                            const uint32_t* d_row_part, const uint32_t* d_row_x, const uint32_t* d_row_of,
+                            const uint32_t* d_ys, const void* d_vals, uint8_t* d_verdicts) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  int rc = check_t(t);
+  if (rc) return rc;
+  if (nack == 0) return HBH_OK;
+  if (!d_commits || !d_row_part || !d_row_x || !d_row_of || !d_ys || !d_vals || !d_verdicts || nrow == 0)
+    return fail(HBH_ERR_ARG, "null pointer");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = dev_stream(e, stream);
+  rc = begin_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(e->work.ensure(nrow * (t + 1) * HBH_G1_BYTES));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, d_commits, d_row_part, d_row_x, e->work.p));
+  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_row_of, d_ys, (const uint32_t*)d_vals, d_verdicts));
+  e->timer.end(s, tm);
+  return end_call(e, s);
 }
 
 }  // extern "C"

@@ -343,6 +343,17 @@ __global__ void __launch_bounds__(256) k_bivar_row(int nrow, int t, const uint32
   g1_jac_to_words(acc, out + (size_t)g * G1_WORDS);
 }
 
+// x_k = idx_k + 1 (threshold_crypto into_fr_plus_1) for device-resident index arrays; an index of
+// 0xffffffff (x would wrap to 0) sets the combine's status to HBL_BAD_INDEX (== HBH_ERR_ARG).
+__global__ void __launch_bounds__(256) k_index_plus_one(int n, int m, const uint32_t* __restrict__ idx,
+                                                        uint32_t* __restrict__ xs, int* __restrict__ status) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t v = idx[k];
+  xs[k] = v + 1u;
+  if (v == 0xffffffffu) status[k / m] = hbl::HBL_BAD_INDEX;
+}
+
 // BivarCommitment::evaluate(x, y) == G1::one() * val  (src/sync_key_gen.rs:542), from the rows
 // R = row(x): evaluate(x, y) = sum_j R_j y^j (Horner with the small y).  One thread per ack.
 __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint32_t* __restrict__ rows,
@@ -447,6 +458,12 @@ hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const u
   if (nack <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_bivar_check, grid_for(nack), dim3(256), 0, s, nack, t, (const uint32_t*)rows, row_idx, ys,
                      vals, verdict);
+  return hipGetLastError();
+}
+
+hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint32_t* xs, int* status) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_index_plus_one, grid_for(n), dim3(256), 0, s, n, m, idx, xs, status);
   return hipGetLastError();
 }
 

@@ -177,9 +177,49 @@ __global__ void __launch_bounds__(256) k_g2_decompress(int n, const uint32_t* __
   ok[i] = valid ? 1 : 0;
 }
 
+// Byte-level half of the decoding on the device, for encodings already in HBM (the _dev entry
+// points): the same flag rules and word reversal as the host's parse_compressed (engine.hip).
+// One thread per encoding of nfe 48-byte big-endian field elements.
+__global__ void __launch_bounds__(256) k_wire_parse(int n, int nfe, const uint8_t* __restrict__ in,
+                                                    uint32_t* __restrict__ xw, uint8_t* __restrict__ flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* b = in + (size_t)i * 48 * nfe;
+  const uint8_t b0 = b[0];
+  uint8_t f = 0;
+  if (!(b0 & 0x80)) {
+    f = hbl::WIRE_REJECT;
+  } else if (b0 & 0x40) {
+    bool zero = (b0 & 0x3f) == 0;
+    for (int k = 1; k < 48 * nfe; k++) zero = zero && b[k] == 0;
+    f = zero ? hbl::WIRE_INFINITY : hbl::WIRE_REJECT;
+  } else if (b0 & 0x20) {
+    f = hbl::WIRE_GREATEST;
+  }
+  for (int c = 0; c < nfe; c++) {
+    const uint8_t* e = b + 48 * (nfe - 1 - c);
+    for (int w = 0; w < 12; w++) {
+      uint32_t v = 0;
+      for (int k = 0; k < 4; k++) {
+        const int pos = 47 - (w * 4 + k);
+        const uint8_t byte = (c == nfe - 1 && pos == 0) ? (uint8_t)(b0 & 0x1f) : e[pos];
+        v |= (uint32_t)byte << (8 * k);
+      }
+      xw[((size_t)i * nfe + c) * 12 + w] = v;
+    }
+  }
+  flags[i] = f;
+}
+
 }  // namespace hb
 
 namespace hbl {
+
+hipError_t wire_parse(hipStream_t s, int n, int nfe, const uint8_t* in, uint32_t* xw, uint8_t* flags) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_wire_parse, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, nfe, in, xw, flags);
+  return hipGetLastError();
+}
 
 hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok) {
   if (n <= 0) return hipSuccess;

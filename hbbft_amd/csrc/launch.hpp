@@ -10,6 +10,7 @@
 namespace hbl {
 
 constexpr int HBL_DUPLICATE = 5;  // == HBH_ERR_DUPLICATE_ENTRY
+constexpr int HBL_BAD_INDEX = 1;  // == HBH_ERR_ARG
 constexpr int MILLER_STEPS = 68;
 constexpr int LINE_Q4 = 21;  // 16-byte chunks per line (3 Fp2 x 14 limbs)
 inline int pad64(size_t n) { return (int)((n + 63) / 64 * 64); }
@@ -79,6 +80,9 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
 // check's part: verdict[a] = (sum_j R[row_idx[a]][j] * y^j == g1 * val[a]).
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
                        const uint32_t* vals, uint8_t* verdict);
+// xs[k] = idx[k] + 1 for n = ncomb * m device-resident indices; status[k / m] = HBL_BAD_INDEX for
+// an index of 0xffffffff (status zeroed by the caller beforehand).
+hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint32_t* xs, int* status);
 // Commitment::evaluate(x) for n (commitment, x) requests; commitments of t+1 G1 points.  out[r].
 hipError_t commit_eval(hipStream_t s, int n, int t, const void* commits, const uint32_t* commit_idx, const uint32_t* xs,
                        void* out);

@@ -19,4 +19,8 @@ hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t
 // G2Compressed::into_affine: xw = 24 words per point (x.c0 then x.c1), out = ABI G2 points.
 hipError_t g2_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok);
 
+// Device-side flag parsing + word reversal of n encodings (nfe = 1 for G1, 2 for G2) already in
+// device memory: xw = 12 * nfe words per point, flags as above.
+hipError_t wire_parse(hipStream_t s, int n, int nfe, const uint8_t* in, uint32_t* xw, uint8_t* flags);
+
 }  // namespace hbl

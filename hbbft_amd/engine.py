@@ -253,6 +253,33 @@ class Engine:
                                           ctypes.cast(out, ctypes.c_void_p)))
         return bytes(out)[:n]
 
+    # ------------------------------------------------------------ device-resident variants
+    # ints are raw device addresses (e.g. torch ``data_ptr()``); stream None = engine stream
+    def interpolate_g1_dev(self, stream, ncomb, t, d_idx, d_pts, d_out, d_status):
+        vp = ctypes.c_void_p
+        check(self._l.hbh_interpolate_g1_dev(self._h, vp(stream) if stream else None, ncomb, t, vp(d_idx), vp(d_pts),
+                                             vp(d_out), vp(d_status)))
+
+    def interpolate_g2_dev(self, stream, ncomb, t, d_idx, d_pts, d_out, d_status):
+        vp = ctypes.c_void_p
+        check(self._l.hbh_interpolate_g2_dev(self._h, vp(stream) if stream else None, ncomb, t, vp(d_idx), vp(d_pts),
+                                             vp(d_out), vp(d_status)))
+
+    def g1_decompress_dev(self, stream, n, d_in, d_out, d_ok):
+        vp = ctypes.c_void_p
+        check(self._l.hbh_g1_decompress_dev(self._h, vp(stream) if stream else None, n, vp(d_in), vp(d_out), vp(d_ok)))
+
+    def g2_decompress_dev(self, stream, n, d_in, d_out, d_ok):
+        vp = ctypes.c_void_p
+        check(self._l.hbh_g2_decompress_dev(self._h, vp(stream) if stream else None, n, vp(d_in), vp(d_out), vp(d_ok)))
+
+    def bivar_ack_check_dev(self, stream, nack, t, d_commits, nrow, d_row_part, d_row_x, d_row_of, d_ys, d_vals,
+                            d_verdicts):
+        vp = ctypes.c_void_p
+        check(self._l.hbh_bivar_ack_check_dev(self._h, vp(stream) if stream else None, nack, t, vp(d_commits), nrow,
+                                              vp(d_row_part), vp(d_row_x), vp(d_row_of), vp(d_ys), vp(d_vals),
+                                              vp(d_verdicts)))
+
     def set_pairing_impl(self, impl):
         """HBH_IMPL_*: 1 = lane-cooperative (six lanes per check), 2 = one thread per check (signed
         limbs, stage kernels), 3 = auto (default), 4 = lane pair (two lanes per check, fused)."""
@@ -335,3 +362,60 @@ def g2_uncompressed_from_abi(b):
     if not any(b):
         return bytes([0x40]) + bytes(191)
     return b[48:96][::-1] + b[0:48][::-1] + b[144:192][::-1] + b[96:144][::-1]
+
+
+class _PoolCalls:
+    """Routes Engine's ``hbh_<op>`` calls to the pool's ``hbh_pool_<op>`` entry points."""
+
+    def __init__(self, lib):
+        self._lib = lib
+
+    def __getattr__(self, name):
+        return getattr(self._lib, name.replace("hbh_engine_", "hbh_", 1).replace("hbh_", "hbh_pool_", 1))
+
+
+class Pool(Engine):
+    """Multi-device fan-out (hbh_pool_*): one engine per shard, the batch split by instance,
+    one host thread per shard, outputs gathered in order.  ``devices`` lists each shard's device
+    (repeat a device for several shards on it).  Offers the batched calls of Engine that have a
+    pool entry point: verify_sig_shares, verify_signatures, verify_dec_shares, combine_verify_g2,
+    interpolate_g1, bivar_ack_check, set_pairing_impl."""
+
+    POOLED = {"verify_sig_shares", "verify_signatures", "verify_dec_shares", "combine_verify_g2",
+              "interpolate_g1", "bivar_ack_check", "set_pairing_impl", "close", "shards", "handle", "device",
+              "shard_engine"}
+
+    def __init__(self, devices):
+        lib = _lib.lib()
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        h = ctypes.c_void_p()
+        check(lib.hbh_pool_create(devs, len(devices), ctypes.byref(h)))
+        self._raw = lib
+        self._l = _PoolCalls(lib)
+        self._h = h
+        self.device = list(devices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._raw.hbh_pool_destroy(self._h)
+            self._h = None
+
+    def shard_engine(self, s):
+        """Borrowed Engine view of shard s (owned by the pool; for profiling counters)."""
+        h = ctypes.c_void_p()
+        check(self._raw.hbh_pool_engine(self._h, int(s), ctypes.byref(h)))
+        e = Engine.__new__(Engine)
+        e._l, e._h, e.device = self._raw, h, self.device[s]
+        e.close = lambda: None
+        return e
+
+    @property
+    def shards(self):
+        n = ctypes.c_int()
+        check(self._raw.hbh_pool_shards(self._h, ctypes.byref(n)))
+        return n.value
+
+    def __getattribute__(self, name):
+        if not name.startswith("_") and name not in Pool.POOLED and hasattr(Engine, name):
+            raise AttributeError("Pool has no pooled entry point for %s" % name)
+        return object.__getattribute__(self, name)

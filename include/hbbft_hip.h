@@ -55,6 +55,55 @@ const char* hbh_last_error(void);
 /* Number of HIP devices visible to this process. */
 int hbh_device_count(int* out);
 
+/* ---------------------------------------------------------------- device-resident variants
+ * Same results as the host-pointer calls, with every array in device memory (HBM) and the call
+ * asynchronous on `stream` (hipStream_t as void*, NULL = engine stream); ordered after the
+ * engine's previous call as hbh_verify_pairing_eq_dev.  Index arrays are not inspected on the host.
+ *   hbh_interpolate_g*_dev: d_idx node indices (x = idx + 1; an index of 0xffffffff gives status
+ *     HBH_ERR_ARG for its combine), d_status written per combine as hbh_interpolate_g*.
+ *   hbh_g*_decompress_dev: compressed encodings in HBM, flags parsed on the device.
+ *   hbh_bivar_ack_check_dev: the caller supplies the row plan -- nrow distinct (part, x) requests
+ *     (d_row_part, d_row_x, part < nparts of d_commits) and d_row_of[a] = the row of ack a -- that
+ *     hbh_bivar_ack_check derives on the host; d_vals = 32-byte LE scalars. */
+int hbh_interpolate_g1_dev(hbh_engine* eng, void* stream, size_t ncomb, int t, const uint32_t* d_idx,
+                           const void* d_pts, void* d_out, int* d_status);
+int hbh_interpolate_g2_dev(hbh_engine* eng, void* stream, size_t ncomb, int t, const uint32_t* d_idx,
+                           const void* d_pts, void* d_out, int* d_status);
+int hbh_g1_decompress_dev(hbh_engine* eng, void* stream, size_t n, const uint8_t* d_in, void* d_out, uint8_t* d_ok);
+int hbh_g2_decompress_dev(hbh_engine* eng, void* stream, size_t n, const uint8_t* d_in, void* d_out, uint8_t* d_ok);
+int hbh_bivar_ack_check_dev(hbh_engine* eng, void* stream, size_t nack, int t, const void* d_commits, size_t nrow,
+                            const uint32_t* d_row_part, const uint32_t* d_row_x, const uint32_t* d_row_of,
+                            const uint32_t* d_ys, const void* d_vals, uint8_t* d_verdicts);
+
+/* ---------------------------------------------------------------- engine pool (multi-device)
+ * One engine per shard; devices[s] is shard s's device (a device may appear more than once: each
+ * shard has its own stream and workspaces).  A pool call splits its batch by INSTANCE (document /
+ * ciphertext / combine / SyncKeyGen part) into contiguous instance ranges of about equal item
+ * counts, runs every shard on its own host thread, and writes verdicts and points back in the
+ * caller's order -- byte-identical to the single-engine call.  No cross-device collective exists
+ * on this path.  Errors: the first failing shard's code, with "shard s: ..." in
+ * hbh_last_error.  Replaces the reference's single synchronous verifier per node
+ * (src/traits.rs:297-336) with a node-wide fan-out over the GPUs of one host. */
+typedef struct hbh_pool hbh_pool;
+int hbh_pool_create(const int* devices, int nshards, hbh_pool** out);
+int hbh_pool_destroy(hbh_pool* pool);
+int hbh_pool_shards(const hbh_pool* pool, int* out);
+int hbh_pool_engine(hbh_pool* pool, int shard, hbh_engine** out);
+int hbh_pool_set_pairing_impl(hbh_pool* pool, int impl);
+int hbh_pool_verify_sig_shares(hbh_pool* pool, size_t n, const uint8_t* pks, const uint8_t* sigs,
+                               const uint8_t* hashes, size_t ndocs, const uint32_t* doc_idx, uint8_t* verdicts);
+int hbh_pool_verify_dec_shares(hbh_pool* pool, size_t n, const uint8_t* shares, const uint8_t* pks,
+                               const uint8_t* huv, const uint8_t* w, size_t ncts, const uint32_t* ct_idx,
+                               uint8_t* verdicts);
+int hbh_pool_combine_verify_g2(hbh_pool* pool, size_t ncomb, int t, const uint32_t* idx, const uint8_t* shares,
+                               const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out, int* status,
+                               uint8_t* verdicts);
+int hbh_pool_interpolate_g1(hbh_pool* pool, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts,
+                            uint8_t* out, int* status);
+int hbh_pool_bivar_ack_check(hbh_pool* pool, size_t nack, int t, size_t nparts, const uint8_t* commits,
+                             const uint32_t* part_idx, const uint32_t* xs, const uint32_t* ys, const uint8_t* vals,
+                             uint8_t* verdicts);
+
 /* ---------------------------------------------------------------- pairing-equality checks
  * Generic batched check  e(P1[i], Q1[q1_idx[i]]) == e(P2[i], Q2[q2_idx[i]])  for i < n,
  * computed as one 2-pair multi-Miller loop + one final exponentiation per item.

@@ -1,0 +1,114 @@
+"""Device-resident entry points (hbh_*_dev): inputs and outputs in HBM (torch tensors), launched on
+a caller stream; byte-identical to the host-pointer calls on the same data, including the error
+statuses (duplicate index, 0xffffffff index) and rejected encodings."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import bls12_381 as C
+from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
+
+pytestmark = pytest.mark.gpu
+R = C.R
+G1 = g1a(C.g1_uncompressed(C.G1_GEN))
+G2 = g2a(C.g2_uncompressed(C.G2_GEN))
+
+
+def dev(b, dtype=torch.uint8):
+    a = np.frombuffer(bytes(b), dtype=np.uint8).copy()
+    t = torch.from_numpy(a).to("cuda:0")
+    return t if dtype == torch.uint8 else t.view(dtype)
+
+
+@pytest.mark.parametrize("g2", [False, True], ids=["g1", "g2"])
+def test_interpolate_dev(engine, g2):
+    rng = random.Random(5 + g2)
+    t, ncomb = 3, 6
+    size = 192 if g2 else 96
+    base = G2 if g2 else G1
+    pts = (engine.g2_mul if g2 else engine.g1_mul)([base] * (ncomb * (t + 1)),
+                                                    [rng.randrange(1, R) for _ in range(ncomb * (t + 1))])
+    idx = [rng.sample(range(20), t + 1) for _ in range(ncomb)]
+    idx[2][1] = idx[2][0]            # duplicate -> HBH_ERR_DUPLICATE_ENTRY
+    want_out, want_st = (engine.interpolate_g2 if g2 else engine.interpolate_g1)(t, idx, pts)
+    d_idx = dev(np.array([i for row in idx for i in row], dtype=np.uint32).tobytes(), torch.int32)
+    d_pts = dev(b"".join(pts))
+    d_out = torch.zeros(ncomb * size, dtype=torch.uint8, device="cuda:0")
+    d_st = torch.full((ncomb,), -1, dtype=torch.int32, device="cuda:0")
+    s = torch.cuda.Stream()
+    fn = engine.interpolate_g2_dev if g2 else engine.interpolate_g1_dev
+    fn(s.cuda_stream, ncomb, t, d_idx.data_ptr(), d_pts.data_ptr(), d_out.data_ptr(), d_st.data_ptr())
+    torch.cuda.synchronize()
+    assert d_st.cpu().tolist() == want_st and want_st[2] == 5
+    out = bytes(d_out.cpu().numpy())
+    for c in range(ncomb):
+        if want_st[c] == 0:
+            assert out[c * size:(c + 1) * size] == want_out[c]
+    # an index of 0xffffffff -> status HBH_ERR_ARG for that combine only
+    bad = np.array([i for row in idx for i in row], dtype=np.uint32)
+    bad[0] = 0xFFFFFFFF
+    d_idx2 = dev(bad.tobytes(), torch.int32)
+    fn(None, ncomb, t, d_idx2.data_ptr(), d_pts.data_ptr(), d_out.data_ptr(), d_st.data_ptr())
+    torch.cuda.synchronize()
+    st = d_st.cpu().tolist()
+    assert st[0] == 1 and st[1:] == want_st[1:]
+
+
+@pytest.mark.parametrize("g2", [False, True], ids=["g1", "g2"])
+def test_decompress_dev(engine, g2):
+    rng = random.Random(8)
+    base = C.G2_GEN if g2 else C.G1_GEN
+    mul = C.g2_mul if g2 else C.g1_mul
+    comp = C.g2_compress if g2 else C.g1_compress
+    encs = [comp(mul(base, rng.randrange(1, R))) for _ in range(5)] + [comp(None)]
+    e = bytearray(encs[0])
+    e[0] &= 0x7F                      # not compressed -> reject
+    encs.append(bytes(e))
+    e = bytearray(encs[1])
+    e[-1] ^= 1                        # probably off-curve -> reject
+    encs.append(bytes(e))
+    want_pts, want_ok = (engine.g2_decompress if g2 else engine.g1_decompress)(encs)
+    n, esz, psz = len(encs), (96 if g2 else 48), (192 if g2 else 96)
+    d_in = dev(b"".join(encs))
+    d_out = torch.zeros(n * psz, dtype=torch.uint8, device="cuda:0")
+    d_ok = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    (engine.g2_decompress_dev if g2 else engine.g1_decompress_dev)(None, n, d_in.data_ptr(), d_out.data_ptr(),
+                                                                   d_ok.data_ptr())
+    torch.cuda.synchronize()
+    assert bytes(d_ok.cpu().numpy()) == want_ok
+    assert bytes(d_out.cpu().numpy()) == b"".join(want_pts)
+    assert want_ok[:6] == b"\x01" * 6 and want_ok[6] == 0
+
+
+def test_bivar_ack_check_dev(engine):
+    rng = random.Random(12)
+    t, nparts = 2, 3
+    npos = (t + 1) * (t + 2) // 2
+    coefs = [rng.randrange(1, R) for _ in range(nparts * npos)]
+    flat = engine.g1_mul([G1] * (nparts * npos), coefs)
+    parts = [flat[p * npos:(p + 1) * npos] for p in range(nparts)]
+    acks = [(p, x, y) for p in range(nparts) for x in (2, 7) for y in range(1, 5)]
+
+    def cp(i, j):
+        return j * (j + 1) // 2 + i if i <= j else i * (i + 1) // 2 + j
+
+    def value(p, x, y):  # BivarPoly::evaluate with the symmetric coefficient layout
+        return sum(coefs[p * npos + cp(i, j)] * pow(x, i, R) * pow(y, j, R)
+                   for i in range(t + 1) for j in range(t + 1)) % R
+
+    vals = [value(*a) if k % 3 else rng.randrange(0, R) for k, a in enumerate(acks)]
+    want = engine.bivar_ack_check(t, parts, [a[0] for a in acks], [a[1] for a in acks], [a[2] for a in acks], vals)
+    rows = list(dict.fromkeys((p, x) for p, x, _ in acks))
+    row_of = [rows.index((p, x)) for p, x, _ in acks]
+    u32 = lambda v: dev(np.array(v, dtype=np.uint32).tobytes(), torch.int32)  # noqa: E731
+    d_commits = dev(b"".join(flat))
+    d_vals = dev(b"".join(v.to_bytes(32, "little") for v in vals))
+    d_v = torch.zeros(len(acks), dtype=torch.uint8, device="cuda:0")
+    rp, rx, ro, ys = u32([r[0] for r in rows]), u32([r[1] for r in rows]), u32(row_of), u32([a[2] for a in acks])
+    engine.bivar_ack_check_dev(None, len(acks), t, d_commits.data_ptr(), len(rows), rp.data_ptr(), rx.data_ptr(),
+                               ro.data_ptr(), ys.data_ptr(), d_vals.data_ptr(), d_v.data_ptr())
+    torch.cuda.synchronize()
+    assert bytes(d_v.cpu().numpy()) == want
+    assert want == bytes(1 if k % 3 else 0 for k in range(len(acks)))

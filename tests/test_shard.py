@@ -1,6 +1,7 @@
-"""N>1 path on CPU: world_size-2 gloo processes shard a batch by index / by instance and gather
-the verdict bytes on rank 0 in the original order (the GPU work is replaced by a deterministic
-per-item function so only the sharding and the host gather are under test)."""
+"""N>1 path on CPU: world_size-2 gloo processes shard the golden ThresholdSign batch
+(tests/golden/threshold_sign_n10_t3.json: 2 documents x 10 shares, forged kinds included) by
+instance, verify their slice with the C oracle (the GPU engine's role on the box), and gather the
+verdict bytes on rank 0 in the original order; the result equals the fixture's verdicts."""
 import os
 import socket
 
@@ -36,29 +37,55 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, q):
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "threshold_sign_n10_t3.json")
+
+
+def _batch():
+    import json
+    with open(GOLDEN) as f:
+        d = json.load(f)
+    items = [(m, s["idx"], bytes.fromhex(s["sig"]), bool(s["valid"])) for m, doc in enumerate(d["docs"])
+             for s in doc["shares"]]
+    return d, items
+
+
+def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    lo, hi = shard_range(n, rank, world)
-    local = bytes((i * 7 + 3) % 2 for i in range(lo, hi))  # stand-in verdicts
-    out = gather_verdicts(local, n)
+    from oracle import cbls
+    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
+    d, items = _batch()
+    inst = np.array([m for m, _, _, _ in items])
+    lo, hi = shard_by_instance(len(items), inst, rank, world)
+    pks = [g1a(bytes.fromhex(h)) for h in d["pk_shares"]]
+    hs = [g2a(bytes.fromhex(doc["hash"])) for doc in d["docs"]]
+    local = bytes(int(cbls.verify_g2(pks[i], g2a(sig), hs[m])) for m, i, sig, _ in items[lo:hi])
+    out = gather_verdicts(local, len(items))
     if rank == 0:
-        q.put(out)
+        q.put((out, [(lo, hi)]))
+    else:
+        q.put((None, [(lo, hi)]))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2])
-def test_gather_verdicts_gloo(world):
-    n = 1000
+def test_shard_by_instance_golden_batch_gloo(world):
+    from oracle import cbls
+    if not os.path.exists(cbls.LIB_PATH):
+        pytest.skip("C oracle not built")
+    _, items = _batch()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = q.get(timeout=120)
+    got = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert out == bytes((i * 7 + 3) % 2 for i in range(n))
+    out = next(o for o, _ in got if o is not None)
+    spans = sorted(sp[0] for _, sp in got)
+    assert spans == [(0, 10), (10, 20)]  # one document per rank, never split
+    assert out == bytes(int(v) for _, _, _, v in items)
