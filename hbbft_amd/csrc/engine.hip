@@ -12,6 +12,8 @@
 
 #include "../../include/hbbft_hip.h"
 #include "launch.hpp"
+#include "interp_pair.hpp"
+#include "lcprep.hpp"
 #include "wire.hpp"
 
 namespace {
@@ -128,8 +130,8 @@ int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, 
     HBH_CHECK(inf1->ensure(n1));
   }
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
-  HBH_CHECK(hbl::g2_prepare(s, (int)n0, d_pts0, coef0.p, (uint8_t*)inf0.p, (int)n1, d_pts1, n1 ? coef1->p : nullptr,
-                            n1 ? (uint8_t*)inf1->p : nullptr));
+  HBH_CHECK(hbl::lc_prep_pair(s, (int)n0, d_pts0, coef0.p, (uint8_t*)inf0.p, (int)n1, d_pts1, n1 ? coef1->p : nullptr,
+                              n1 ? (uint8_t*)inf1->p : nullptr));
   e->timer.end(s, t);
   return HBH_OK;
 }
@@ -489,6 +491,21 @@ int run_mul(hbh_engine* e, size_t n, const uint8_t* pts, size_t pt_bytes, const 
   return HBH_OK;
 }
 
+// G2 combines: few combines (latency-bound: the chip is idle but for the serial chains) take the
+// lane-pair form (k_interp_digits + k_interp_pair); many take k_interp_endo (throughput form).
+constexpr size_t INTERP_PAIR_MAX = 64;
+int launch_combine_g2(hbh_engine* e, hipStream_t s, size_t ncomb, size_t m, const uint32_t* d_xs, const void* d_pts,
+                      void* d_out, int* d_status) {
+  if (ncomb <= INTERP_PAIR_MAX && hbl::interp_g2_pair_fits((int)m)) {
+    HBH_CHECK(e->in_d.ensure(ncomb * m * 4 * sizeof(uint64_t)));
+    HBH_CHECK(hbl::interp_digits(s, (int)ncomb, (int)m, d_xs, (uint64_t*)e->in_d.p, d_status));
+    HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)e->in_d.p, d_pts, d_out));
+    return HBH_OK;
+  }
+  HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, d_xs, d_pts, d_out, d_status));
+  return HBH_OK;
+}
+
 int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out, int* status,
                bool g2) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
@@ -519,12 +536,13 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
   HBH_CHECK(hipMemcpyAsync(e->in_b.p, pts, ncomb * m * pb, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  if (g2)
-    HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
-                              (int*)e->status.p));
-  else
+  if (g2) {
+    rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p);
+    if (rc) return rc;
+  } else {
     HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
                               (int*)e->status.p));
+  }
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * pb, hipMemcpyDeviceToHost, s));
   HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -595,8 +613,8 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
   HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p12.data(), p12.size(), hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
-                            (int*)e->status.p));
+  rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p);
+  if (rc) return rc;
   e->timer.end(s, tm);
   rc = run_pairing_dev(e, s, ncomb, e->in_p1.p, e->in_q1.p, ncomb, nullptr, nullptr, e->out_x.p, ncomb, nullptr, 1,
                        (uint8_t*)e->out_v.p);
@@ -858,9 +876,10 @@ int run_interp_dev(hbh_engine* e, void* stream, size_t ncomb, int t, const uint3
   HBH_CHECK(hipMemsetAsync(d_status, 0, ncomb * sizeof(int), s));
   HBH_CHECK(hbl::index_plus_one(s, (int)(ncomb * m), (int)m, d_idx, (uint32_t*)e->in_a.p, d_status));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  if (g2)
-    HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status));
-  else
+  if (g2) {
+    rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status);
+    if (rc) return rc;
+  } else
     HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status));
   e->timer.end(s, tm);
   return end_call(e, s);

@@ -7,6 +7,7 @@
 
 #include "curve.hpp"
 #include "fr.hpp"
+#include "interp_pair.hpp"
 #include "launch.hpp"
 
 namespace hb {
@@ -319,6 +320,58 @@ __global__ void __launch_bounds__(256) k_interp_endo(int ncomb, int m, const uin
   }
 }
 
+// ------------------------------------------------------------------ interpolate(), lane-pair form
+// Stage 1 of the latency form of the G2 combine (k_interp_pair.hip does the curve work): the four
+// 64-bit GLS digits of every lambda_k(0) (the endo_term split), digits[(c*m + k)*4 + j].  One
+// workgroup per combine; a duplicate x sets status[c] = HBL_DUPLICATE and zero digits (terms = O).
+__global__ void __launch_bounds__(64) k_interp_digits(int ncomb, int m, const uint32_t* __restrict__ xs,
+                                                      uint64_t* __restrict__ digits, int* __restrict__ status) {
+  extern __shared__ unsigned char smem_raw[];
+  __shared__ int s_dup;
+  Fr* snum = reinterpret_cast<Fr*>(smem_raw);
+  Fr* sden = snum + m;
+  Fr* slam = sden + m;
+  const int c = blockIdx.x;
+  if (c >= ncomb) return;
+  const uint32_t* cx = xs + (size_t)c * m;
+  if (threadIdx.x == 0) s_dup = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < m; k += blockDim.x) {
+    Fr num, den;
+    if (!lagrange_parts(cx, m, k, num, den)) s_dup = 1;
+    snum[k] = num;
+    sden[k] = den;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_dup) {
+      status[c] = hbl::HBL_DUPLICATE;
+      for (int k = 0; k < m; k++)
+        for (int w = 0; w < FRL; w++) slam[k].l[w] = 0;
+    } else {
+      slam[0] = sden[0];
+      for (int k = 1; k < m; k++) slam[k] = fr_mul(slam[k - 1], sden[k]);
+      Fr inv = fr_inv_vartime(slam[m - 1]);
+      for (int k = m - 1; k > 0; k--) {
+        const Fr ik = fr_mul(inv, slam[k - 1]);
+        inv = fr_mul(inv, sden[k]);
+        slam[k] = fr_to_canon(fr_mul(snum[k], ik));
+      }
+      slam[0] = fr_to_canon(fr_mul(snum[0], inv));
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < m; k += blockDim.x) {
+    uint64_t q[4];
+    k_to_u64(slam[k].l, q);
+    uint64_t* d = digits + ((size_t)c * m + k) * 4;
+    d[0] = div_x_abs(q);
+    d[1] = div_x_abs(q);
+    d[2] = div_x_abs(q);
+    d[3] = q[0];
+  }
+}
+
 // ------------------------------------------------------------------ SyncKeyGen
 // BivarCommitment::row(x)[i] = sum_j C[coeff_pos(i,j)] x^j, by Horner in G1 with the small
 // integer x (src/sync_key_gen.rs:496): t steps of (x * acc + C) instead of (t+1) full scalar
@@ -464,6 +517,13 @@ hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const u
 hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint32_t* xs, int* status) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_index_plus_one, grid_for(n), dim3(256), 0, s, n, m, idx, xs, status);
+  return hipGetLastError();
+}
+
+hipError_t interp_digits(hipStream_t s, int ncomb, int m, const uint32_t* xs, uint64_t* digits, int* status) {
+  if (ncomb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_interp_digits, dim3((unsigned)ncomb), dim3(64), (size_t)3 * m * sizeof(hb::Fr), s, ncomb, m,
+                     xs, digits, status);
   return hipGetLastError();
 }
 

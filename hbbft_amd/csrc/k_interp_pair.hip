@@ -1,0 +1,215 @@
+// Latency form of the G2 Lagrange combine (PublicKeySet::combine_signatures,
+// src/threshold_sign.rs:249-259, for the one document of combine_and_verify_sig): the curve work of
+// k_interp_endo on LANE PAIRS.  Two lanes hold the c0 / c1 components of every Fp2 coordinate
+// (pfp.hpp), so each Fp2 product is one lane-pair product (x*y + z*w per lane) instead of three
+// serial Fp products: the serial chain that bounds a single combine's latency runs about twice as
+// fast.  The work split is the one of k_interp_endo: term (k, j) = digit chunk s of GLS digit j of
+// lambda_k(0) times psi^j(P_k) (sign (-1)^j), 32-bit chunks, one lane pair per (chunk, term); an LDS
+// tree sums each chunk's terms; pair 0 joins the two chunk sums by Horner and writes the affine
+// result.  Formulas: dbl-2009-l, add-2007-bl, madd-2007-bl (curve.hpp), the same group law, so the
+// affine output is byte-identical.  Digits come from k_interp_digits (k_curve.hip).
+#define HS_MULFN static __device__ __noinline__
+#include "interp_pair.hpp"
+#include "launch.hpp"
+#include "pfp.hpp"
+#include "words.hpp"
+
+namespace hbs {
+
+constexpr int IP_THREADS = 512;          // 256 lane pairs per combine
+constexpr int IP_NCHUNK = 2;             // 32-bit chunks of the 64-bit digits
+constexpr int IP_PAIRS = IP_THREADS / 2;
+constexpr int IP_G = IP_PAIRS / IP_NCHUNK;  // lane pairs per chunk (power of two)
+constexpr int IP_WORDS = 3 * NL;         // one lane's Jacobian point (x, y, z own components)
+
+HP_D bool hj_is_zero(const HJac& p) { return h_is_zero(p.z); }
+HP_D HJac hj_zero() { return {h_one(), h_one(), h_zero()}; }
+HP_D HJac hj_reduce(const HJac& p) { return {fp_reduce(p.x), fp_reduce(p.y), fp_reduce(p.z)}; }
+
+// dbl-2009-l; inputs |.| < 2p, outputs reduced
+HP_D HJac hj_dbl(const HJac& p) {
+  const Fp A = h_sqr(p.x);
+  const Fp B = h_sqr(p.y);
+  const Fp C = h_sqr(B);
+  const Fp D = fp_reduce(fp_lin(2, fp_sub(fp_sub(h_sqr(fp_add(p.x, B)), A), C), 0, C));
+  const Fp E = fp_lin(3, A, 0, A);
+  const Fp F = h_sqr(E);
+  HJac r;
+  r.x = fp_reduce(fp_sub(F, fp_add(D, D)));
+  r.y = fp_reduce(fp_sub(h_mul(E, fp_sub(D, r.x)), fp_lin(8, C, 0, C)));
+  const Fp yz = h_mul(p.y, p.z);
+  r.z = fp_reduce(fp_add(yz, yz));
+  return r;
+}
+
+// add-2007-bl (general), exceptional cases as curve.hpp jac_add; conditions are pair-uniform
+HP_D HJac hj_add(const HJac& p, const HJac& q) {
+  if (hj_is_zero(p)) return q;
+  if (hj_is_zero(q)) return p;
+  const Fp Z1Z1 = h_sqr(p.z);
+  const Fp Z2Z2 = h_sqr(q.z);
+  const Fp U1 = h_mul(p.x, Z2Z2);
+  const Fp U2 = h_mul(q.x, Z1Z1);
+  const Fp S1 = h_mul(h_mul(p.y, q.z), Z2Z2);
+  const Fp S2 = h_mul(h_mul(q.y, p.z), Z1Z1);
+  const Fp H = fp_reduce(fp_sub(U2, U1));
+  const Fp rr = fp_reduce(fp_lin(2, S2, -2, S1));
+  if (h_is_zero(H)) {
+    if (h_is_zero(rr)) return hj_dbl(p);
+    return hj_zero();
+  }
+  const Fp I = h_sqr(fp_add(H, H));
+  const Fp J = h_mul(H, I);
+  const Fp V = h_mul(U1, I);
+  HJac r;
+  r.x = fp_reduce(fp_sub(fp_sub(h_sqr(rr), J), fp_add(V, V)));
+  const Fp SJ = h_mul(S1, J);
+  r.y = fp_reduce(fp_sub(h_mul(rr, fp_sub(V, r.x)), fp_add(SJ, SJ)));
+  r.z = fp_reduce(h_mul(fp_sub(fp_sub(h_sqr(fp_add(p.z, q.z)), Z1Z1), Z2Z2), H));
+  return r;
+}
+
+// madd-2007-bl: p + (x2, y2), the affine point not infinity
+HP_D HJac hj_add_affine(const HJac& p, const Fp& x2, const Fp& y2) {
+  if (hj_is_zero(p)) return {x2, y2, h_one()};
+  const Fp Z1Z1 = h_sqr(p.z);
+  const Fp U2 = h_mul(x2, Z1Z1);
+  const Fp S2 = h_mul(h_mul(y2, p.z), Z1Z1);
+  const Fp H = fp_reduce(fp_sub(U2, p.x));
+  const Fp rr = fp_reduce(fp_lin(2, S2, -2, p.y));
+  if (h_is_zero(H)) {
+    if (h_is_zero(rr)) return hj_dbl(p);
+    return hj_zero();
+  }
+  const Fp HH = h_sqr(H);
+  const Fp I = fp_lin(4, HH, 0, HH);
+  const Fp J = h_mul(H, I);
+  const Fp V = h_mul(p.x, I);
+  HJac r;
+  r.x = fp_reduce(fp_sub(fp_sub(h_sqr(rr), J), fp_add(V, V)));
+  const Fp YJ = h_mul(p.y, J);
+  r.y = fp_reduce(fp_sub(h_mul(rr, fp_sub(V, r.x)), fp_add(YJ, YJ)));
+  r.z = fp_reduce(fp_sub(fp_sub(h_sqr(fp_add(p.z, H)), Z1Z1), HH));
+  return r;
+}
+
+// k * (x, y) for a 32-bit k, double-and-add from the top set bit (jac_mul_affine)
+HP_D HJac hj_mul_affine(const Fp& x, const Fp& y, bool inf, uint32_t k) {
+  HJac acc = hj_zero();
+  if (inf || k == 0) return acc;
+  const int top = 31 - __builtin_clz(k);
+  acc = {x, y, h_one()};
+#pragma unroll 1
+  for (int i = top - 1; i >= 0; i--) {
+    acc = hj_dbl(acc);
+    if ((k >> i) & 1) acc = hj_add_affine(acc, x, y);
+  }
+  return acc;
+}
+
+// psi on own components: psi(x) = conj(x) * (0 + c u) -> (x1 c, x0 c); psi(y) = conj(y) * c2
+HP_D Fp psi_xh(const Fp& x) { return fp_reduce(fp_mul(dpp_fp<DPP_SWAP>(x), fp_const(hb::PSI_C1_C1))); }
+HP_D Fp psi_yh(const Fp& y) { return fp_reduce(h_mul(h_conj(y), h_const(hb::PSI_C2_C0, hb::PSI_C2_C1))); }
+
+// 1 / a in Fp2 with a variable-time inverse of the (public) norm: both lanes invert the same norm
+HP_D Fp h_inv_vartime(const Fp& a) {
+  const Fp s = fp_sqr(a);
+  const Fp n = fp_add(s, dpp_fp<DPP_SWAP>(s));
+  uint32_t w[12], p[12], r[12];
+  fp_to_words(n, w);
+#pragma unroll
+  for (int i = 0; i < 12; i++) p[i] = hb::PM2_W[i];
+  p[0] += 2;  // p - 2 + 2
+  hb::words_inv_vartime<12>(w, p, r);
+  return h_conj(fp_mul(a, fp_from_words(r)));
+}
+
+HP_D void lds_put(uint32_t* s, const HJac& p) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    s[i] = (uint32_t)p.x.l[i];
+    s[NL + i] = (uint32_t)p.y.l[i];
+    s[2 * NL + i] = (uint32_t)p.z.l[i];
+  }
+}
+HP_D HJac lds_get(const uint32_t* s) {
+  HJac p;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    p.x.l[i] = (int32_t)s[i];
+    p.y.l[i] = (int32_t)s[NL + i];
+    p.z.l[i] = (int32_t)s[2 * NL + i];
+  }
+  return p;
+}
+
+__global__ void __launch_bounds__(IP_THREADS) k_interp_pair(int ncomb, int m, const uint64_t* __restrict__ digits,
+                                                            const uint32_t* __restrict__ pts, uint32_t* __restrict__ out) {
+  extern __shared__ uint32_t sm[];  // IP_THREADS x IP_WORDS, lane-major
+  const int c = blockIdx.x;
+  if (c >= ncomb) return;  // uniform per workgroup
+  const int pair = threadIdx.x >> 1, chunk = pair / IP_G, g = pair % IP_G;
+  HJac acc = hj_zero();
+  for (int t = g; t < m * 4; t += IP_G) {
+    const int k = t >> 2, j = t & 3;
+    const uint32_t* w = pts + ((size_t)c * m + k) * 48;
+    const bool inf = lp_both(words_zero(w + (lp_even() ? 0 : 12), 12) && words_zero(w + (lp_even() ? 24 : 36), 12));
+    Fp x, y;
+    h_g2_load(w, x, y);
+    for (int s = 0; s < j; s++) {
+      x = psi_xh(x);
+      y = psi_yh(y);
+    }
+    if (j & 1) y = fp_neg(y);
+    const uint64_t d = digits[((size_t)c * m + k) * 4 + j];
+    const uint32_t kc = (uint32_t)(d >> (32 * chunk));
+    acc = hj_add(acc, hj_mul_affine(x, y, inf, kc));
+  }
+  uint32_t* mine = sm + (size_t)threadIdx.x * IP_WORDS;
+  lds_put(mine, acc);
+  __syncthreads();
+  for (int s = IP_G / 2; s > 0; s >>= 1) {
+    if (g < s) {
+      acc = hj_add(lds_get(mine), lds_get(sm + (size_t)(threadIdx.x + 2 * s) * IP_WORDS));
+      lds_put(mine, acc);
+    }
+    __syncthreads();
+  }
+  if (pair != 0) return;
+  // R = 2^32 S_1 + S_0
+  HJac r = lds_get(sm + (size_t)(IP_G * 2 + (threadIdx.x & 1)) * IP_WORDS);
+#pragma unroll 1
+  for (int b = 0; b < 32; b++) r = hj_dbl(r);
+  r = hj_add(r, lds_get(sm + (size_t)(threadIdx.x & 1) * IP_WORDS));
+  uint32_t* o = out + (size_t)c * 48 + (lp_even() ? 0 : 12);
+  if (hj_is_zero(r)) {
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      o[i] = 0u;
+      o[24 + i] = 0u;
+    }
+    return;
+  }
+  const Fp zi = h_inv_vartime(fp_reduce(r.z));
+  const Fp zi2 = h_sqr(zi);
+  const Fp xa = h_mul(r.x, zi2);
+  const Fp ya = h_mul(r.y, h_mul(zi2, zi));
+  fp_to_words(xa, o);
+  fp_to_words(ya, o + 24);
+}
+
+}  // namespace hbs
+
+namespace hbl {
+
+bool interp_g2_pair_fits(int m) { return m >= 1 && m <= 512; }
+
+hipError_t interp_g2_pair(hipStream_t s, int ncomb, int m, const uint64_t* digits, const void* pts, void* out) {
+  if (ncomb <= 0) return hipSuccess;
+  const size_t lds = (size_t)hbs::IP_THREADS * hbs::IP_WORDS * 4;
+  hipLaunchKernelGGL(hbs::k_interp_pair, dim3((unsigned)ncomb), dim3(hbs::IP_THREADS), lds, s, ncomb, m, digits,
+                     (const uint32_t*)pts, (uint32_t*)out);
+  return hipGetLastError();
+}
+
+}  // namespace hbl

@@ -119,20 +119,41 @@ struct PairSide {
   uint32_t nq;          // number of Q points / tables
 };
 
+// Register budget (2 waves per SIMD = 256 VGPRs per lane): a side whose P is the generator (GEN)
+// keeps no P in registers -- the line evaluation multiplies by constants -- and a walked side keeps
+// only T: Q itself is re-read from memory at the 5 addition steps instead of living in 28 VGPRs
+// through the 63 doublings.
 struct SideState {
-  Fp xP, yP;      // P (Montgomery), both lanes
+  Fp xP, yP;      // P (Montgomery), both lanes (unused when GEN)
   bool act;       // pair contributes (P != O and Q != O)
+  bool qinf;      // WALK: Q is the point at infinity (the walk runs from (1, 1), masked out)
   uint32_t q;     // Q index
   HJac T;         // WALK: the running multiple of Q (own components)
-  Fp xQ, yQ;      // WALK: Q (own components)
 };
 
-template <bool WALK>
+template <bool GEN>
+HP_D Fp side_xP(const SideState& st) { return GEN ? fp_const(hb::G1X_M) : st.xP; }
+template <bool GEN>
+HP_D Fp side_yP(const SideState& st, bool negate) {
+  return GEN ? (negate ? fp_neg(fp_const(hb::G1Y_M)) : fp_const(hb::G1Y_M)) : st.yP;
+}
+
+HP_D void side_q(const PairSide& s, const SideState& st, Fp& xQ, Fp& yQ) {
+  h_g2_load(s.q + (size_t)st.q * 48, xQ, yQ);
+  if (st.qinf) {
+    xQ = h_one();
+    yQ = h_one();
+  }
+}
+
+template <bool WALK, bool GEN>
 HP_D bool side_init(const PairSide& s, int i, bool negate, SideState& st) {
   st.q = s.idx ? s.idx[i] : (uint32_t)i;
   if (st.q >= s.nq) return false;
   bool pinf;
-  if (s.p) {
+  if (GEN) {
+    pinf = false;
+  } else if (s.p) {
     const uint32_t* w = s.p + (size_t)i * 24;
     pinf = words_zero(w, 24);
     st.xP = fp_from_words(w);
@@ -142,30 +163,32 @@ HP_D bool side_init(const PairSide& s, int i, bool negate, SideState& st) {
     st.xP = fp_const(hb::G1X_M);
     st.yP = fp_const(hb::G1Y_M);
   }
-  if (negate) st.yP = fp_neg(st.yP);
-  bool qinf;
+  if (!GEN && negate) st.yP = fp_neg(st.yP);
   if (WALK) {
     const uint32_t* w = s.q + (size_t)st.q * 48;
-    qinf = lp_both(words_zero(w + (lp_even() ? 0 : 12), 12) && words_zero(w + (lp_even() ? 24 : 36), 12));
-    h_g2_load(w, st.xQ, st.yQ);
-    if (qinf) {  // dummy walk from (1, 1): the pair is masked out
-      st.xQ = h_one();
-      st.yQ = h_one();
-    }
-    st.T = {st.xQ, st.yQ, h_one()};
+    st.qinf = lp_both(words_zero(w + (lp_even() ? 0 : 12), 12) && words_zero(w + (lp_even() ? 24 : 36), 12));
+    Fp xQ, yQ;
+    side_q(s, st, xQ, yQ);  // dummy walk from (1, 1) when Q = O: the pair is masked out
+    st.T = {xQ, yQ, h_one()};
   } else {
-    qinf = s.qinf[st.q] != 0;
+    st.qinf = s.qinf[st.q] != 0;
   }
-  st.act = !pinf && !qinf;
+  st.act = !pinf && !st.qinf;
   return true;
 }
 
 // multiply the side's line of this step into f
-template <bool WALK, bool DBL>
-HP_D H12 side_line(const H12& f, const PairSide& s, SideState& st, int step) {
+template <bool WALK, bool GEN, bool DBL>
+HP_D H12 side_line(const H12& f, const PairSide& s, SideState& st, int step, bool negate) {
   HLine l;
   if (WALK) {
-    l = DBL ? h_dbl_step(st.T) : h_add_step(st.T, st.xQ, st.yQ);
+    if (DBL) {
+      l = h_dbl_step(st.T);
+    } else {
+      Fp xQ, yQ;
+      side_q(s, st, xQ, yQ);
+      l = h_add_step(st.T, xQ, yQ);
+    }
   } else {
     const int4* p = s.lines + ((size_t)(st.q * PAIR_STEPS + step) * 2 + (lp_even() ? 0 : 1)) * PL_Q4;
     int32_t w[4 * PL_Q4];
@@ -182,8 +205,8 @@ HP_D H12 side_line(const H12& f, const PairSide& s, SideState& st, int step) {
     }
   }
   const Fp c0 = st.act ? l.c0 : h_one();
-  const Fp c1 = st.act ? fp_mul(l.c1, st.xP) : fp_zero();
-  const Fp c4 = st.act ? fp_mul(l.c4, st.yP) : fp_zero();
+  const Fp c1 = st.act ? fp_mul(l.c1, side_xP<GEN>(st)) : fp_zero();
+  const Fp c4 = st.act ? fp_mul(l.c4, side_yP<GEN>(st, negate)) : fp_zero();
   return h12_mul_014(f, c0, c1, c4);
 }
 
@@ -195,14 +218,17 @@ struct PairArgs {
   uint32_t* value_out;  // 144 canonical words per check (may be null)
 };
 
-template <bool W1, bool W2>
+// GEN: 0 = both P read per check, 1 = P1 is the generator, 2 = P2 is the generator
+template <bool W1, bool W2, int GEN>
 __global__ void __launch_bounds__(256, 2) k_pair_verify(PairArgs a) {
   extern __shared__ uint32_t stash_lds[];
   const int i = (int)((blockIdx.x * 256u + threadIdx.x) >> 1);
   if (i >= a.n) return;  // both lanes of a pair leave together
+  constexpr bool G1 = GEN == 1, G2 = GEN == 2;
+  const bool neg2 = (a.flags & 1) != 0;
   SideState A, B;
-  const bool ok1 = side_init<W1>(a.s1, i, false, A);
-  const bool ok2 = side_init<W2>(a.s2, i, (a.flags & 1) != 0, B);
+  const bool ok1 = side_init<W1, G1>(a.s1, i, false, A);
+  const bool ok2 = side_init<W2, G2>(a.s2, i, neg2, B);
   if (!ok1 || !ok2) {  // index out of range: reject, never read past a table
     if (lp_even() && a.verdict) a.verdict[i] = 0;
     return;
@@ -212,12 +238,12 @@ __global__ void __launch_bounds__(256, 2) k_pair_verify(PairArgs a) {
 #pragma unroll 1
   for (int b = 62; b >= 0; b--) {
     if (b != 62) f = h12_sqr(f);
-    f = side_line<W1, true>(f, a.s1, A, step);
-    f = side_line<W2, true>(f, a.s2, B, step);
+    f = side_line<W1, G1, true>(f, a.s1, A, step, false);
+    f = side_line<W2, G2, true>(f, a.s2, B, step, neg2);
     step++;
     if ((hb::X_ABS >> b) & 1) {
-      f = side_line<W1, false>(f, a.s1, A, step);
-      f = side_line<W2, false>(f, a.s2, B, step);
+      f = side_line<W1, G1, false>(f, a.s1, A, step, false);
+      f = side_line<W2, G2, false>(f, a.s2, B, step, neg2);
       step++;
     }
   }
@@ -309,14 +335,27 @@ hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairS
   const dim3 grid((unsigned)((2 * (size_t)n + 255) / 256)), block(256);
   const size_t lds = (size_t)hbs::STASH_WORDS * 256 * 4;
   const bool w1 = d1.lines == nullptr, w2 = d2.lines == nullptr;
-  if (w1 && w2)
-    hipLaunchKernelGGL((hbs::k_pair_verify<true, true>), grid, block, lds, s, a);
-  else if (w1)
-    hipLaunchKernelGGL((hbs::k_pair_verify<true, false>), grid, block, lds, s, a);
-  else if (w2)
-    hipLaunchKernelGGL((hbs::k_pair_verify<false, true>), grid, block, lds, s, a);
+  // a null P on exactly one side selects the generator instantiation; both null keeps the
+  // run-time generator path of side_init (P1 and P2 held in registers)
+  const int gen = (d1.p == nullptr) == (d2.p == nullptr) ? 0 : (d1.p == nullptr ? 1 : 2);
+#define HBS_PAIR_LAUNCH(G)                                                                 \
+  do {                                                                                     \
+    if (w1 && w2)                                                                          \
+      hipLaunchKernelGGL((hbs::k_pair_verify<true, true, G>), grid, block, lds, s, a);     \
+    else if (w1)                                                                           \
+      hipLaunchKernelGGL((hbs::k_pair_verify<true, false, G>), grid, block, lds, s, a);    \
+    else if (w2)                                                                           \
+      hipLaunchKernelGGL((hbs::k_pair_verify<false, true, G>), grid, block, lds, s, a);    \
+    else                                                                                   \
+      hipLaunchKernelGGL((hbs::k_pair_verify<false, false, G>), grid, block, lds, s, a);   \
+  } while (0)
+  if (gen == 1)
+    HBS_PAIR_LAUNCH(1);
+  else if (gen == 2)
+    HBS_PAIR_LAUNCH(2);
   else
-    hipLaunchKernelGGL((hbs::k_pair_verify<false, false>), grid, block, lds, s, a);
+    HBS_PAIR_LAUNCH(0);
+#undef HBS_PAIR_LAUNCH
   return hipGetLastError();
 }
 
