@@ -35,6 +35,7 @@ SIGNATURES = [
     ("hbh_combine_verify_g2", _I, [_P, _SZ, _I, _P, _P, _P, _P, _P, _P, _P]),
     ("hbh_g1_mul", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_g2_mul", _I, [_P, _SZ, _P, _P, _P]),
+    ("hbh_g1_mul_gen", _I, [_P, _SZ, _P, _P]),
     ("hbh_bivar_row", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),
     ("hbh_g1_decompress", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_g2_decompress", _I, [_P, _SZ, _P, _P, _P]),

@@ -94,7 +94,8 @@ struct hbh_engine {
   // stream can never overwrite tables another stream's kernels are still reading.
   hipEvent_t done = nullptr;
   // workspaces
-  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep;
+  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep, fbtab;
+  bool fbtab_ready = false;  // fixed-base comb table of g1 (built on first use)
   size_t g1rep_n = 0;
   // staging for host-pointer entry points
   DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
@@ -491,6 +492,15 @@ int run_mul(hbh_engine* e, size_t n, const uint8_t* pts, size_t pt_bytes, const 
   return HBH_OK;
 }
 
+// The g1 comb table, built on the engine stream the first time a call needs it.
+int ensure_fbtab(hbh_engine* e, hipStream_t s) {
+  if (e->fbtab_ready) return HBH_OK;
+  HBH_CHECK(e->fbtab.ensure(hbl::fb_table_bytes()));
+  HBH_CHECK(hbl::fb_table(s, e->fbtab.p));
+  e->fbtab_ready = true;
+  return HBH_OK;
+}
+
 // G2 combines: few combines (latency-bound: the chip is idle but for the serial chains) take the
 // lane-pair form (k_interp_digits + k_interp_pair); many take k_interp_endo (throughput form).
 constexpr size_t INTERP_PAIR_MAX = 64;
@@ -839,7 +849,10 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
   HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, e->in_a.p, d_rp, d_rx, e->work.p));
-  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, (uint8_t*)e->out_v.p));
+  rc = ensure_fbtab(e, s);
+  if (rc) return rc;
+  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
+                             (uint8_t*)e->out_v.p));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, nack, hipMemcpyDeviceToHost, s));
   {
@@ -944,9 +957,43 @@ int hbh_bivar_ack_check_dev(hbh_engine* e, void* stream, size_t nack, int t, con
   HBH_CHECK(e->work.ensure(nrow * (t + 1) * HBH_G1_BYTES));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
   HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, d_commits, d_row_part, d_row_x, e->work.p));
-  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_row_of, d_ys, (const uint32_t*)d_vals, d_verdicts));
+  rc = ensure_fbtab(e, s);
+  if (rc) return rc;
+  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_row_of, d_ys, (const uint32_t*)d_vals, e->fbtab.p,
+                             d_verdicts));
   e->timer.end(s, tm);
   return end_call(e, s);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// out[i] = g1 * k_i from the comb table: Poly::commitment / BivarPoly::commitment and public-key
+// derivation (src/sync_key_gen.rs:346-357, 508; network_info.rs:59-62).
+int hbh_g1_mul_gen(hbh_engine* e, size_t n, const uint8_t* scalars, uint8_t* out) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (n == 0) return HBH_OK;
+  if (!scalars || !out) return fail(HBH_ERR_ARG, "null pointer");
+  if (n > (size_t)1 << 28) return fail(HBH_ERR_ARG, "batch too large");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  int rc = begin_call(e, s);
+  if (rc) return rc;
+  rc = ensure_fbtab(e, s);
+  if (rc) return rc;
+  HBH_CHECK(e->in_a.ensure(n * 32));
+  HBH_CHECK(e->out_x.ensure(n * HBH_G1_BYTES));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, scalars, n * 32, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::g1_mul_gen(s, (int)n, e->fbtab.p, (const uint32_t*)e->in_a.p, e->out_x.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, n * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  rc = end_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
 }
 
 }  // extern "C"

@@ -54,6 +54,49 @@ __global__ void __launch_bounds__(256) k_g2_mul(int n, const uint32_t* __restric
   g2_jac_to_words(jac_mul_affine(x, y, inf, k), out + (size_t)i * G2_WORDS);
 }
 
+// ------------------------------------------------------------------ fixed-base g1 * k
+// Comb table of the G1 generator: FB_TAB[w][d] = d * 2^(8w) * g1 (affine words), w < 32, 1 <= d < 256
+// (row d = 0 unused).  g1 * k is then 32 mixed additions of table points -- no doublings -- instead
+// of ~255 doublings + ~128 additions: the public commitments of BivarPoly::commitment /
+// Poly::commitment (src/sync_key_gen.rs:346-357, 508) and the g1 * val side of every Ack check
+// (:542).  784 KiB per engine, built once on first use.
+constexpr int FB_WINDOWS = 32;
+constexpr int FB_ROW = 256;
+
+__global__ void __launch_bounds__(256) k_fb_table(uint32_t* __restrict__ tab) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= FB_WINDOWS * FB_ROW) return;
+  const int w = g / FB_ROW, d = g % FB_ROW;
+  uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int bit = 8 * w;
+  k[bit >> 5] = (uint32_t)d << (bit & 31);
+  g1_jac_to_words(jac_mul_affine(fp_const(G1X_M), fp_const(G1Y_M), false, k), tab + (size_t)g * G1_WORDS);
+}
+
+// acc + g1 * k from the comb table (k: 8 LE words)
+__device__ __forceinline__ Jac<Fp> fb_mul(const uint32_t* __restrict__ tab, const uint32_t* k) {
+  Jac<Fp> acc = jac_zero<Fp>();
+#pragma unroll 1
+  for (int w = 0; w < FB_WINDOWS; w++) {
+    const uint32_t d = (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
+    if (d == 0) continue;
+    Fp x, y;
+    bool inf;
+    load_g1(tab + ((size_t)w * FB_ROW + d) * G1_WORDS, x, y, inf);
+    acc = jac_add_affine(acc, x, y);
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) k_g1_mul_gen(int n, const uint32_t* __restrict__ tab,
+                                                    const uint32_t* __restrict__ scalars, uint32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  for (int j = 0; j < 8; j++) k[j] = scalars[(size_t)i * 8 + j];
+  g1_jac_to_words(fb_mul(tab, k), out + (size_t)i * G1_WORDS);
+}
+
 // ------------------------------------------------------------------ interpolate()
 // lambda_k(0) = prod_{j != k} x_j / (x_j - x_k) over Fr (threshold_crypto interpolate, SURVEY
 // Appendix B.6), then term_k = lambda_k * sample_k.  One thread per (combine, sample).
@@ -412,7 +455,7 @@ __global__ void __launch_bounds__(256) k_index_plus_one(int n, int m, const uint
 __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint32_t* __restrict__ rows,
                                                      const uint32_t* __restrict__ row_idx,
                                                      const uint32_t* __restrict__ ys, const uint32_t* __restrict__ vals,
-                                                     uint8_t* __restrict__ verdict) {
+                                                     const uint32_t* __restrict__ fbtab, uint8_t* __restrict__ verdict) {
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= nack) return;
   const uint32_t* R = rows + (size_t)row_idx[a] * (t + 1) * G1_WORDS;
@@ -427,7 +470,7 @@ __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint
   }
   uint32_t k[8];
   for (int j = 0; j < 8; j++) k[j] = vals[(size_t)a * 8 + j];
-  const Jac<Fp> w = jac_mul_affine(fp_const(G1X_M), fp_const(G1Y_M), false, k);
+  const Jac<Fp> w = fb_mul(fbtab, k);
   verdict[a] = jac_eq(acc, w) ? 1 : 0;
 }
 
@@ -507,10 +550,21 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
   return hipGetLastError();
 }
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
-                       const uint32_t* vals, uint8_t* verdict) {
+                       const uint32_t* vals, const void* fbtab, uint8_t* verdict) {
   if (nack <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_bivar_check, grid_for(nack), dim3(256), 0, s, nack, t, (const uint32_t*)rows, row_idx, ys,
-                     vals, verdict);
+                     vals, (const uint32_t*)fbtab, verdict);
+  return hipGetLastError();
+}
+
+size_t fb_table_bytes() { return (size_t)hb::FB_WINDOWS * hb::FB_ROW * hb::G1_WORDS * 4; }
+hipError_t fb_table(hipStream_t s, void* tab) {
+  hipLaunchKernelGGL(hb::k_fb_table, grid_for(hb::FB_WINDOWS * hb::FB_ROW), dim3(256), 0, s, (uint32_t*)tab);
+  return hipGetLastError();
+}
+hipError_t g1_mul_gen(hipStream_t s, int n, const void* tab, const uint32_t* scalars, void* out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_g1_mul_gen, grid_for(n), dim3(256), 0, s, n, (const uint32_t*)tab, scalars, (uint32_t*)out);
   return hipGetLastError();
 }
 

@@ -78,8 +78,14 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
                      void* out);
 // BivarCommitment::evaluate(x, y) == g1 * val for nack checks, given the rows R = row(x) of each
 // check's part: verdict[a] = (sum_j R[row_idx[a]][j] * y^j == g1 * val[a]).
+// fbtab: the fixed-base comb table of g1 (fb_table), used for the g1 * val side.
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
-                       const uint32_t* vals, uint8_t* verdict);
+                       const uint32_t* vals, const void* fbtab, uint8_t* verdict);
+// Fixed-base comb table of the G1 generator (32 windows x 256 affine points, fb_table_bytes()) and
+// out[i] = g1 * k_i from it (32 mixed additions per scalar).
+size_t fb_table_bytes();
+hipError_t fb_table(hipStream_t s, void* tab);
+hipError_t g1_mul_gen(hipStream_t s, int n, const void* tab, const uint32_t* scalars, void* out);
 // xs[k] = idx[k] + 1 for n = ncomb * m device-resident indices; status[k / m] = HBL_BAD_INDEX for
 // an index of 0xffffffff (status zeroed by the caller beforehand).
 hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint32_t* xs, int* status);

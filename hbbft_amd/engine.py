@@ -192,6 +192,16 @@ class Engine:
     def g2_mul(self, pts, scalars):
         return self._mul(self._l.hbh_g2_mul, G2_BYTES, pts, scalars)
 
+    def g1_mul_gen(self, scalars):
+        """g1 * k for each scalar from the fixed-base comb table (hbh_g1_mul_gen)."""
+        sb = b"".join(int(k).to_bytes(32, "little") for k in scalars)
+        n = len(scalars)
+        out = (ctypes.c_uint8 * max(n * G1_BYTES, 1))()
+        keep = buf(sb)
+        check(self._l.hbh_g1_mul_gen(self._h, n, keep[1], ctypes.cast(out, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [raw[i * G1_BYTES:(i + 1) * G1_BYTES] for i in range(n)]
+
     def bivar_row(self, t, commits, part_idx, xs):
         """BivarCommitment::row(x) (src/sync_key_gen.rs:496) for each (part, x)."""
         cb = _join([c for part in commits for c in part], G1_BYTES)

@@ -4,7 +4,7 @@ Same message types (``Part``, ``Ack``), outcomes (``PartOutcome`` / ``AckOutcome
 (``PartFault`` / ``AckFault``, ``sync_key_gen.rs:551-588``) and state rules (``ProposalState``,
 ``is_complete``, ``is_ready``, ``generate``) as the reference.  Where the crypto runs:
 
-  GPU (engine, public data)   BivarCommitment::row (hbh_bivar_row), Poly::commitment (hbh_g1_mul of
+  GPU (engine, public data)   BivarCommitment::row (hbh_bivar_row), Poly::commitment (hbh_g1_mul_gen of
                               g1), BivarPoly::commitment, Ciphertext::verify (hbh_verify_ciphertexts),
                               BivarCommitment::evaluate == g1 * val (hbh_bivar_ack_check)
   host (secrets, hashing)     SecretKey::decrypt's U * sk and XOR stream, encrypt_with_rng,
@@ -219,7 +219,7 @@ class SyncKeyGen:
         t = threshold
         ncoef = (t + 1) * (t + 2) // 2
         coeffs = [rng.randrange(0, R_ORDER) for _ in range(ncoef)]
-        commit = engine.g1_mul([G1_GEN] * ncoef, coeffs)
+        commit = engine.g1_mul_gen(coeffs)
         rows = []
         for i in range(len(kg.pub_keys)):
             x = i + 1
@@ -282,7 +282,7 @@ class SyncKeyGen:
             plain = _decrypt_batch(self.engine, self.sec_key, [p.rows[self.our_idx] for _, p, _ in new], self.threads)
             polys = [de_row(b, t + 1) if b is not None else None for b in plain]
             flat = [c for poly in polys if poly is not None for c in poly]
-            comm = self.engine.g1_mul([G1_GEN] * len(flat), flat) if flat else []
+            comm = self.engine.g1_mul_gen(flat) if flat else []
             k = 0
             for j, (sidx, part, st) in enumerate(new):
                 if plain[j] is None:

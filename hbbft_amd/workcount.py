@@ -86,8 +86,9 @@ def g1_mul_small(k):
     return _add(_scale(G1_DBL, k.bit_length() - 1), _scale(G1_ADD, bin(k).count("1") - 1))
 
 
-def bivar_ack(t, y, val_bits=255, val_weight=128):
+def bivar_ack(t, y, val_windows=32):
     """k_bivar_check for one ack: Horner over the t+1 row points with the small y, then g1 * val
-    (jac_mul_affine: val_bits doublings, val_weight mixed additions) and a cross-multiplied compare."""
+    from the fixed-base comb table (one mixed addition per nonzero byte of val: 32 windows) and a
+    cross-multiplied compare."""
     horner = _scale(_add(g1_mul_small(y), G1_MADD), t + 1)
-    return _add(horner, _scale(G1_DBL, val_bits), _scale(G1_MADD, val_weight), (4, 2))
+    return _add(horner, _scale(G1_MADD, val_windows), (4, 2))

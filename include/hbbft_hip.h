@@ -183,6 +183,10 @@ int hbh_combine_verify_g2(hbh_engine* eng, size_t ncomb, int t, const uint32_t* 
  * host in the reference flow (sign_g2 / decrypt_share). */
 int hbh_g1_mul(hbh_engine* eng, size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out);
 int hbh_g2_mul(hbh_engine* eng, size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_t* out);
+/* out[i] = g1 * k_i with a fixed-base comb table of the generator (32 mixed additions per scalar,
+ * table built on the engine's first use): BivarPoly::commitment / Poly::commitment
+ * (src/sync_key_gen.rs:346-357, 508) and key derivation.  Same points as hbh_g1_mul(g1, k). */
+int hbh_g1_mul_gen(hbh_engine* eng, size_t n, const uint8_t* scalars, uint8_t* out);
 
 /* ---------------------------------------------------------------- SyncKeyGen commitments
  * commits: nparts BivarCommitments of degree t, each (t+1)(t+2)/2 G1 points in threshold_crypto's

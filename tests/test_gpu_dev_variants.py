@@ -112,3 +112,16 @@ def test_bivar_ack_check_dev(engine):
     torch.cuda.synchronize()
     assert bytes(d_v.cpu().numpy()) == want
     assert want == bytes(1 if k % 3 else 0 for k in range(len(acks)))
+
+
+def test_g1_mul_gen_fixed_base(engine):
+    """hbh_g1_mul_gen (comb table of g1) equals hbh_g1_mul(g1, k) and the C oracle, edge scalars
+    included (0 -> infinity, r - 1, r, 2^256 - 1, single-window values)."""
+    from oracle import cbls
+    rng = random.Random(77)
+    ks = [0, 1, 2, 255, 256, 1 << 248, R - 1, R, R + 5, (1 << 256) - 1] + [rng.randrange(0, 1 << 256) for _ in range(500)]
+    got = engine.g1_mul_gen(ks)
+    assert got == engine.g1_mul([G1] * len(ks), ks)
+    assert got[0] == bytes(96) and got[R and 7] == bytes(96)
+    for k, g in list(zip(ks, got))[:12]:
+        assert g == cbls.g1_mul(G1, k % R)
