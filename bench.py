@@ -45,8 +45,8 @@ MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2
 IMPLS = {"lane_coop": 1, "thread_signed": 2, "auto": 3, "pair": 4}   # HBH_IMPL_* (include/hbbft_hip.h)
 KERNEL_NAMES = {"lane_coop": "hbs::k_lc_* (miller+easy+exp+glue+verdict)",
                 "thread_signed": "hbs::k_ts_* (miller+easy+exp+glue+verdict)",
-                "pair": "hbs::k_pair_verify<false,true>",
-                "auto": "hbs::k_pair_verify<false,true>"}
+                "pair": "hbs::k_pair_verify<false, true, 2>",
+                "auto": "hbs::k_pair_verify<false, true, 2>"}
 G1_UNC = bytes.fromhex(
     "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
     "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
@@ -112,7 +112,7 @@ def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_sim
     e = {"kernel": kernel, "launches": launches, "avg_launch_ms": avg_ms, "units_per_launch": units,
          "unit": unit_name, "fp_ops_per_unit": op[0], "fp_sqr_per_unit": op[1], "mad_per_unit": mad,
          "achieved": achieved, "peak": MAD_PEAK_MEASURED, "frac": achieved / MAD_PEAK_MEASURED,
-         "peak_theoretical": MAD_PEAK_THEORETICAL}
+         "peak_theoretical": MAD_PEAK_THEORETICAL, "traffic": pmc_traffic(kernel)}
     if waves_per_simd:
         ceil = MAD_CEILING_BY_WAVES.get(waves_per_simd)
         if ceil is None:  # below one wave per SIMD on average: the 1-wave ceiling scaled by occupancy
@@ -491,7 +491,7 @@ def run_decrypt(args, eng, world, rank, dev):
     want = eng.g1_mul(us, [coeffs[0]] * len(mine))
     ok = ok and out == want and all(x == 0 for x in st)
     if rank == 0:
-        main_k = roofline_entry("hbs::k_pair_verify<false,false>", pair_n, pair_ms / max(pair_n, 1), n,
+        main_k = roofline_entry("hbs::k_pair_verify<false, false, 0>", pair_n, pair_ms / max(pair_n, 1), n,
                                 workcount.PAIR_CHECK_TABLE, "decryption-share check", pair_waves_per_simd(n))
         kernels = [main_k]
         if prep_n:
@@ -509,7 +509,7 @@ def run_decrypt(args, eng, world, rank, dev):
             "combines_per_s_rank0": len(mine) / comb_s,                 # host-to-host, one call
             "combines_per_s_rank0_device": len(mine) / (comb_dev_ms / 1e3),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
-                             traffic=pmc_traffic("hbs::k_pair_verify<false,false>"), kernels=kernels,
+                             traffic=pmc_traffic("hbs::k_pair_verify<false, false, 0>"), kernels=kernels,
                              note="both G2 sides (H_uv, W) are per-ciphertext line tables: per check = 2-pair "
                                   "Miller + final exp (workcount.PAIR_CHECK_TABLE)"),
         }

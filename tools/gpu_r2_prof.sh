@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/$TAG
+O=$R/gpurun_out/prof/$TAG
 mkdir -p $O
 B="$R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-combine $*"
 cd /tmp
@@ -13,9 +13,4 @@ timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- python3 $B > $O/fetch.log 2>&1 || { echo "fetch failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- python3 $B > $O/write.log 2>&1 || { echo "write failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU --output-format csv -d $O/sq -o run -- python3 $B > $O/sq.log 2>&1 || { echo "sq failed"; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_WAVES --output-format csv -d $O/sq2 -o run -- python3 $B > $O/sq2.log 2>&1 || { echo "sq2 failed"; tail -3 $O/sq2.log; }
-cat $O/trace/*/run_kernel_stats.csv | head -12
-python3 $R/tools/pmc_summary.py $O/sq | grep -A9 "k_pair"
-python3 $R/tools/pmc_summary.py $O/sq2 | grep -A9 "k_pair"
-python3 $R/tools/pmc_summary.py $O/fetch | grep -A2 "k_pair"
-python3 $R/tools/pmc_summary.py $O/write | grep -A2 "k_pair"
+echo "== $TAG"; head -6 $O/trace/run_kernel_stats.csv | cut -c1-160

@@ -4,7 +4,7 @@ import collections, csv, glob, sys
 root = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
-for f in glob.glob(f"{root}/*/run_counter_collection.csv"):
+for f in glob.glob(f"{root}/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
         disp[k].add((f, r["Dispatch_Id"]))

@@ -1,57 +1,51 @@
-"""HBM traffic of one pairing stage (HBH_IMPL_THREAD_SIGNED, one 65,536-check step) from rocprofv3
---pmc FETCH_SIZE / WRITE_SIZE passes (separate runs), with the gfx950 correction of
-MI355X_MICROARCH.md (FETCH_SIZE counts half the bytes of wide coalesced reads: doubled).
-usage: python tools/pmc_traffic.py gpurun_out/<tag>/pmc profiles/r01/pmc_traffic.json"""
+"""Per-kernel HBM traffic from rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) plus the kernel-trace
+average duration, as profiles/<round>/pmc_traffic.json (read by bench.py's roofline "traffic").
+FETCH_SIZE is doubled (gfx950: it tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM
+section); both counters are in KiB per dispatch.
+usage: pmc_traffic.py OUT.json DIR [DIR ...]   (each DIR holds fetch/ write/ trace/ of one bench)"""
 import collections
 import csv
 import glob
 import json
+import os
 import sys
 
-STAGE = {"hbs::k_ts_miller": 1, "hbs::k_ts_easy": 1, "hbs::k_ts_exp": 5, "hbs::k_ts_glue": 2, "hbs::k_ts_verdict": 1}
-CHECKS = 65536
-# algorithmic bytes per check: P1 (96) + P2 (96) + verdict (1) + the per-check G2 line table read (68 lines x 84 words
-# x 4 B = 22,848 B; the shared per-document H table is read once per 64 checks: 357 B/check)
-ALGO_PER_CHECK = 96 + 96 + 1 + 22848 + 22848 // 64
+
+def norm(name):
+    n = name.split("(")[0]
+    return n[5:] if n.startswith("void ") else n
 
 
-def per_dispatch(root, counter):
-    tot, n = collections.defaultdict(float), collections.defaultdict(set)
-    for f in glob.glob(f"{root}/*/run_counter_collection.csv"):
+def counters(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-            tot[k] += float(r["Counter_Value"])
-            n[k].add((f, r["Dispatch_Id"]))
-    return {k: tot[k] / len(n[k]) for k in tot}
+            k = norm(r["Kernel_Name"])
+            disp[k].add(r["Dispatch_Id"])
+            acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-def main():
-    root, out = sys.argv[1], sys.argv[2]
-    fetch = per_dispatch(root, "FETCH_SIZE")   # KB
-    write = per_dispatch(root, "WRITE_SIZE")   # KB
-    f_raw = sum(fetch.get(k, 0.0) * c for k, c in STAGE.items()) * 1024
-    w = sum(write.get(k, 0.0) * c for k, c in STAGE.items()) * 1024
-    res = {
-        "kernel": "hbs::k_ts_* (one pairing stage: miller + easy + 5 exp + 2 glue + verdict)",
-        "checks_per_launch": CHECKS,
-        "FETCH_SIZE_bytes_raw": f_raw,
-        "FETCH_SIZE_bytes_gfx950_x2": 2 * f_raw,
-        "WRITE_SIZE_bytes": w,
-        "hbm_bytes_per_launch": 2 * f_raw + w,
-        "algorithmic_bytes_per_launch": ALGO_PER_CHECK * CHECKS,
-        "prepare": {"kernel": "hb::k_g2_prepare", "FETCH_SIZE_bytes_gfx950_x2": 2 * fetch.get("hb::k_g2_prepare", 0) * 1024,
-                    "WRITE_SIZE_bytes": write.get("hb::k_g2_prepare", 0) * 1024},
-        "per_kernel_KB": {k: {"FETCH_SIZE": fetch.get(k), "WRITE_SIZE": write.get(k)} for k in STAGE},
-        "source": root,
-        "note": "Fp12 state crosses HBM between the stage kernels (6 x 14 x 4 x 2 B per check per hand-over) and the "
-                "256V+256A-register kernels spill to scratch; traffic / algorithmic shows both",
-    }
-    with open(out, "w") as f:
-        json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1))
-
-
-if __name__ == "__main__":
-    main()
+out = {"kernels": {}, "note": "bytes per launch; FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE; KiB counters x1024"}
+for d in sys.argv[2:]:
+    fetch, write = counters(os.path.join(d, "fetch")), counters(os.path.join(d, "write"))
+    sq = counters(os.path.join(d, "sq"))
+    dur = {}
+    for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            dur[norm(r["Name"])] = float(r["AverageNs"])
+    for k in fetch:
+        fb = fetch[k].get("FETCH_SIZE", 0.0) * 1024 * 2
+        wb = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        e = {"fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
+             "avg_ns": dur.get(k), "source": os.path.basename(os.path.normpath(d))}
+        if k in sq:
+            e["sq"] = sq[k]
+            w = sq[k].get("SQ_WAVE_CYCLES")
+            if w:
+                e["sq_wait_any_frac"] = sq[k].get("SQ_WAIT_ANY", 0.0) / w
+        out["kernels"][k] = e
+json.dump(out, open(sys.argv[1], "w"), indent=1)
+print(json.dumps({k: {"hbm_MB": round(v["hbm_bytes_per_launch"] / 1e6, 2), "avg_ms": (v["avg_ns"] or 0) / 1e6,
+                      "wait": round(v.get("sq_wait_any_frac", -1), 3)} for k, v in out["kernels"].items()}, indent=1))
