@@ -326,3 +326,32 @@ def test_g2_decompress_matches_oracle(engine):
     assert list(ok) == want_ok
     assert got == want_pts
     assert sum(want_ok) == 10 and len(encs) == 18
+
+
+def test_subgroup_contract_wire_path(engine):
+    """The ABI's subgroup contract (include/hbbft_hip.h, Conventions): points reach the engine only
+    through subgroup-checked decoding, as threshold_crypto's deserialisation guarantees.  On-curve
+    points outside the prime-order subgroup (G1 and G2) are rejected by hbh_g*_decompress, so they
+    can never feed the GLS/GLV-split combines or the pairing checks; subgroup points decode and
+    combine to the C oracle's bytes."""
+    rng = random.Random(1234)
+    for g2, dec, comp in ((False, engine.g1_decompress, C.g1_compress), (True, engine.g2_decompress, C.g2_compress)):
+        nfe = 2 if g2 else 1
+        outside = []
+        while len(outside) < 3:
+            b = b"".join(rng.randrange(C.P).to_bytes(48, "big") for _ in range(nfe))
+            e = bytes([b[0] | 0x80]) + b[1:]
+            try:
+                (C.g2_decompress if g2 else C.g1_decompress)(e)
+            except C.DecodeError as err:
+                if "subgroup" in str(err):
+                    outside.append(e)
+        base = C.G2_GEN if g2 else C.G1_GEN
+        inside = [comp((C.g2_mul if g2 else C.g1_mul)(base, rng.randrange(1, C.R))) for _ in range(3)]
+        pts, ok = dec(outside + inside)
+        assert list(ok) == [0, 0, 0, 1, 1, 1]
+        assert pts[:3] == [bytes(192 if g2 else 96)] * 3
+        idx = [[0, 1, 2]]
+        out, st = (engine.interpolate_g2 if g2 else engine.interpolate_g1)(2, idx, [pts[3:]])
+        assert st == [0]
+        assert out[0] == (cbls.combine_g2 if g2 else cbls.combine_g1)(2, idx[0], pts[3:])[1]
