@@ -125,3 +125,69 @@ def test_g1_mul_gen_fixed_base(engine):
     assert got[0] == bytes(96) and got[R and 7] == bytes(96)
     for k, g in list(zip(ks, got))[:12]:
         assert g == cbls.g1_mul(G1, k % R)
+
+
+def _sign_batch(engine, rng, ndocs, per_doc):
+    from oracle import tc
+    coeffs = [rng.randrange(1, R) for _ in range(3)]
+    sks = [tc.poly_eval(coeffs, i + 1) for i in range(per_doc)]
+    pks = engine.g1_mul([G1] * per_doc, sks)
+    hs = engine.g2_mul([G2] * ndocs, [rng.randrange(1, R) for _ in range(ndocs)])
+    n = ndocs * per_doc
+    bad = set(rng.sample(range(n), n // 7))
+    sigs = engine.g2_mul([hs[i // per_doc] for i in range(n)],
+                         [rng.randrange(1, R) if i in bad else sks[i % per_doc] for i in range(n)])
+    want = bytes(0 if i in bad else 1 for i in range(n))
+    return ([pks[i % per_doc] for i in range(n)], sigs, hs, [i // per_doc for i in range(n)], want)
+
+
+def test_dev_calls_on_two_streams(engine):
+    """Two hbh_verify_pairing_eq_dev calls queued back-to-back on two different streams:
+    the second call's line tables must not overwrite the first call's while its kernels still read
+    them -- the engine orders calls with its completion event.  Both verdict arrays are exact."""
+    from hbbft_amd._lib import IMPL_AUTO, IMPL_PAIR
+    rng = random.Random(2024)
+    batches = [_sign_batch(engine, rng, 64, 32), _sign_batch(engine, rng, 48, 32)]
+    engine.set_pairing_impl(IMPL_PAIR)
+    try:
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        keep, outs = [], []
+        torch.cuda.synchronize()
+        for (pks, sigs, hs, di, want), s in zip(batches, streams):
+            d_pk, d_sg, d_h = dev(b"".join(pks)), dev(b"".join(sigs)), dev(b"".join(hs))
+            d_di = dev(np.array(di, dtype=np.uint32).tobytes(), torch.int32)
+            d_v = torch.zeros(len(want), dtype=torch.uint8, device="cuda:0")
+            engine.verify_pairing_eq_dev(s.cuda_stream, len(want), d_pk.data_ptr(), d_h.data_ptr(), len(hs),
+                                         d_di.data_ptr(), None, d_sg.data_ptr(), len(want), None, d_v.data_ptr())
+            keep += [d_pk, d_sg, d_h, d_di]
+            outs.append((d_v, want))
+        torch.cuda.synchronize()
+        for d_v, want in outs:
+            assert bytes(d_v.cpu().numpy()) == want
+    finally:
+        engine.set_pairing_impl(IMPL_AUTO)
+
+
+def test_dev_index_out_of_range_rejects(engine):
+    """HBH_IMPL_PAIR validates device index arrays in-kernel: an index >= its table size gives
+    verdict 0 for that item only (never a read past the table)."""
+    from hbbft_amd._lib import IMPL_AUTO, IMPL_PAIR
+    rng = random.Random(9)
+    pks, sigs, hs, di, want = _sign_batch(engine, rng, 8, 16)
+    di = list(di)
+    di[5] = 8          # == table size
+    di[77] = 1 << 30   # far out of range
+    engine.set_pairing_impl(IMPL_PAIR)
+    try:
+        d_pk, d_sg, d_h = dev(b"".join(pks)), dev(b"".join(sigs)), dev(b"".join(hs))
+        d_di = dev(np.array(di, dtype=np.uint32).tobytes(), torch.int32)
+        d_v = torch.full((len(want),), 7, dtype=torch.uint8, device="cuda:0")
+        engine.verify_pairing_eq_dev(None, len(want), d_pk.data_ptr(), d_h.data_ptr(), len(hs), d_di.data_ptr(),
+                                     None, d_sg.data_ptr(), len(want), None, d_v.data_ptr())
+        torch.cuda.synchronize()
+        got = bytes(d_v.cpu().numpy())
+    finally:
+        engine.set_pairing_impl(IMPL_AUTO)
+    exp = bytearray(want)
+    exp[5] = exp[77] = 0
+    assert got == bytes(exp)
