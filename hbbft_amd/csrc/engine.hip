@@ -93,6 +93,13 @@ struct hbh_engine {
   // on its own stream before touching the engine-owned workspaces, so a _dev call on a caller
   // stream can never overwrite tables another stream's kernels are still reading.
   hipEvent_t done = nullptr;
+  // HBH_IMPL_PAIR device-pointer calls alternate between two table slots, each with its own
+  // completion event: consecutive calls on different streams then overlap (one call's verify tail
+  // with the next call's table walk and first waves) without sharing a workspace.  Every other
+  // call waits for both slots and records both.
+  hipEvent_t slot_done[2] = {nullptr, nullptr};
+  int slot = 0;
+  DevBuf ptab[2][2], pinf[2][2];
   // workspaces
   DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep, fbtab;
   bool fbtab_ready = false;  // fixed-base comb table of g1 (built on first use)
@@ -108,10 +115,14 @@ using hbl::line_table_bytes;
 // Start of a call on stream s: order it after the engine's previous call.
 int begin_call(hbh_engine* e, hipStream_t s) {
   HBH_CHECK(hipStreamWaitEvent(s, e->done, 0));
+  HBH_CHECK(hipStreamWaitEvent(s, e->slot_done[0], 0));
+  HBH_CHECK(hipStreamWaitEvent(s, e->slot_done[1], 0));
   return HBH_OK;
 }
 int end_call(hbh_engine* e, hipStream_t s) {
   HBH_CHECK(hipEventRecord(e->done, s));
+  HBH_CHECK(hipEventRecord(e->slot_done[0], s));
+  HBH_CHECK(hipEventRecord(e->slot_done[1], s));
   return HBH_OK;
 }
 
@@ -146,10 +157,10 @@ int resolve_impl(const hbh_engine* e, size_t n) {
 // table (k_pair_prep); every other side is walked inside the verify kernel.
 int launch_pair(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
                 const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2, int flags,
-                uint8_t* d_v, uint32_t* d_value) {
+                uint8_t* d_v, uint32_t* d_value, int slot) {
   hbl::PairSideDesc sd[2] = {{d_p1, d_q1, nullptr, nullptr, d_i1, nq1}, {d_p2, d_q2, nullptr, nullptr, d_i2, nq2}};
-  DevBuf* tab[2] = {&e->coef1, &e->coef2};
-  DevBuf* inf[2] = {&e->inf1, &e->inf2};
+  DevBuf* tab[2] = {&e->ptab[slot][0], &e->ptab[slot][1]};
+  DevBuf* inf[2] = {&e->pinf[slot][0], &e->pinf[slot][1]};
   for (int k = 0; k < 2; k++) {
     if (!sd[k].idx || sd[k].nq * 4 > n) continue;
     HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
@@ -192,11 +203,12 @@ int launch_prepared(hbh_engine* e, hipStream_t s, int impl, size_t n, const void
 // the G1 generator for every check.  flags as hbl::pair_verify.
 int run_pairing_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
                     const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2,
-                    int flags, uint8_t* d_v, uint32_t* d_value = nullptr) {
+                    int flags, uint8_t* d_v, uint32_t* d_value = nullptr, int slot = 0) {
   if (n == 0) return HBH_OK;
   if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
   const int impl = resolve_impl(e, n);
-  if (impl == HBH_IMPL_PAIR) return launch_pair(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value);
+  if (impl == HBH_IMPL_PAIR)
+    return launch_pair(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value, slot);
   if (!d_p1 || !d_p2) {
     const void* g = nullptr;
     int rc = g1_repeated(e, s, n, &g);
@@ -314,6 +326,10 @@ int hbh_engine_create(int device, hbh_engine** out) {
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
   if (err == hipSuccess) err = hipEventRecord(e->done, e->stream);
+  for (int k = 0; k < 2 && err == hipSuccess; k++) {
+    err = hipEventCreateWithFlags(&e->slot_done[k], hipEventDisableTiming);
+    if (err == hipSuccess) err = hipEventRecord(e->slot_done[k], e->stream);
+  }
   if (err != hipSuccess) {
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -327,13 +343,18 @@ int hbh_engine_destroy(hbh_engine* e) {
   if (!e) return HBH_OK;
   (void)hipSetDevice(e->device);
   (void)hipEventSynchronize(e->done);
+  for (hipEvent_t ev : e->slot_done)
+    if (ev) (void)hipEventSynchronize(ev);
   (void)hipStreamSynchronize(e->stream);
   e->timer.clear();
   for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->lc0, &e->lc1, &e->lc2, &e->lc3,
-                    &e->g1rep, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v, &e->in_a,
-                    &e->in_b, &e->in_c, &e->in_d, &e->out_x})
+                    &e->g1rep, &e->fbtab, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
+                    &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
+                    &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1]})
     b->release();
   (void)hipEventDestroy(e->done);
+  for (hipEvent_t ev : e->slot_done)
+    if (ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
   delete e;
   return HBH_OK;
@@ -358,6 +379,17 @@ int hbh_verify_pairing_eq_dev(hbh_engine* e, void* stream, size_t n, const void*
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  if (n && resolve_impl(e, n) == HBH_IMPL_PAIR) {
+    // table slot of its own: wait for the last general call and for this slot's previous user only
+    const int slot = e->slot;
+    e->slot ^= 1;
+    HBH_CHECK(hipStreamWaitEvent(s, e->done, 0));
+    HBH_CHECK(hipStreamWaitEvent(s, e->slot_done[slot], 0));
+    int rc = run_pairing_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, 1, d_v, nullptr, slot);
+    if (rc) return rc;
+    HBH_CHECK(hipEventRecord(e->slot_done[slot], s));
+    return HBH_OK;
+  }
   int rc = begin_call(e, s);
   if (rc) return rc;
   rc = run_pairing_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, 1, d_v);
