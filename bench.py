@@ -121,6 +121,32 @@ class Workload:
         self.hash_table = b"".join(self.hashes)
 
 
+def timed_steps(step, streams, steps, world, dev):
+    """Time `steps` calls of step(k) (k-th call on streams[k % len]) with HIP events: start on
+    stream 0 (the others wait for it), end on stream 0 after waiting for the others; barrier +
+    synchronize on both sides; max over ranks.  Returns ms per step."""
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(streams[0])
+    for st in streams[1:]:
+        st.wait_event(ev0)
+    for k in range(steps):
+        step(k)
+    for st in streams[1:]:
+        e = torch.cuda.Event()
+        e.record(st)
+        streams[0].wait_event(e)
+    ev1.record(streams[0])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ms = ev0.elapsed_time(ev1)
+    return (allreduce_max(ms, dev) if world > 1 else ms) / steps
+
+
 def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_simd=None):
     """One kernel's roofline: achieved = units per launch x algorithmic MADs per unit (workcount,
     300 per Fp-mul, 222 per Fp-sqr) / average launch time (HIP events on the engine's stream)."""
@@ -357,26 +383,7 @@ def main():
         raise SystemExit("verdict mismatch against the construction")
     for k in range(args.warmup):
         step(k)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(streams[0])
-    for st in streams[1:]:
-        st.wait_event(ev0)
-    for k in range(args.steps):
-        step(k)
-    for st in streams[1:]:
-        e = torch.cuda.Event()
-        e.record(st)
-        streams[0].wait_event(e)
-    ev1.record(streams[0])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    ms = ev0.elapsed_time(ev1)
-    ms_step = (allreduce_max(ms, dev) if world > 1 else ms) / args.steps
+    ms_step = timed_steps(step, streams, args.steps, world, dev)
     value = n * world / (ms_step / 1e3)
     ok = ok and verdicts_ok()
     # roofline: isolated launches on one stream (no overlap), HIP events around each launch
@@ -480,34 +487,34 @@ def run_decrypt(args, eng, world, rank, dev):
     d_h = to_dev(b"".join(huv))
     d_w = to_dev(b"".join(ws))
     d_ci = torch.from_numpy((inst[lo:hi] - clo).astype(np.int32)).to(dev)
-    d_v = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
-    ts = torch.cuda.Stream(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+    d_vs = [torch.zeros(max(n, 1), dtype=torch.uint8, device=dev) for _ in streams]
     torch.cuda.synchronize(dev)
 
-    def step():
-        eng.verify_pairing_eq_dev(ts.cuda_stream, n, d_d.data_ptr(), d_h.data_ptr(), len(mine), d_ci.data_ptr(),
-                                  d_pk.data_ptr(), d_w.data_ptr(), len(mine), d_ci.data_ptr(), d_v.data_ptr())
+    def step(k=0):
+        eng.verify_pairing_eq_dev(streams[k % len(streams)].cuda_stream, n, d_d.data_ptr(), d_h.data_ptr(), len(mine),
+                                  d_ci.data_ptr(), d_pk.data_ptr(), d_w.data_ptr(), len(mine), d_ci.data_ptr(),
+                                  d_vs[k % len(streams)].data_ptr())
 
-    step()
+    def verdicts_ok():
+        return all(bool((d.cpu().numpy()[:n] == expected).all()) for d in d_vs)
+
+    for k in range(len(streams)):
+        step(k)
     torch.cuda.synchronize(dev)
-    ok = bool((d_v.cpu().numpy()[:n] == expected).all())
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    ok = verdicts_ok()
+    for k in range(args.warmup):
+        step(k)
+    ms_step = timed_steps(step, streams, args.steps, world, dev)
     from hbbft_amd._lib import STAGE_PAIRING, STAGE_PREPARE
-    eng.set_profiling(True)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(ts)
-    for _ in range(args.steps):
-        step()
-    ev1.record(ts)
+    eng.set_profiling(True)   # roofline: isolated single-stream launches
+    for _ in range(max(2, min(args.steps, 5))):
+        step(0)
     torch.cuda.synchronize(dev)
     pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
     prep_ms, prep_n = eng.stage_time(STAGE_PREPARE)
     eng.set_profiling(False)
-    ms_step = _max_over_ranks(ev0.elapsed_time(ev1), world, dev) / args.steps
+    ok = ok and verdicts_ok()
     # combines: first t+1 valid shares per ciphertext -> g = U * msk
     cidx, cpts = [], []
     for j, c in enumerate(mine):
@@ -538,7 +545,7 @@ def run_decrypt(args, eng, world, rank, dev):
             "unit": "shares/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
             "data": "synthetic, seeded (H_uv synthetic in G2; 1/64 invalid shares)",
-            "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total,
+            "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total, "streams": len(streams),
                        "ciphertexts": ncts, "parallelism": "shard-by-ciphertext x%d" % world},
             "verdicts_ok": ok, "combines_ok": out == want,
             "combines_per_s_rank0": len(mine) / comb_s,                 # host-to-host, one call

@@ -100,6 +100,9 @@ struct hbh_engine {
   hipEvent_t slot_done[2] = {nullptr, nullptr};
   int slot = 0;
   DevBuf ptab[2][2], pinf[2][2];
+  // host staging of combine digits (kept alive until the call's stream synchronises)
+  std::vector<uint64_t> h_digits;
+  std::vector<int> h_status;
   // workspaces
   DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep, fbtab;
   bool fbtab_ready = false;  // fixed-base comb table of g1 (built on first use)
@@ -533,14 +536,160 @@ int ensure_fbtab(hbh_engine* e, hipStream_t s) {
   return HBH_OK;
 }
 
+// ---- host Fr (4 x 64-bit Montgomery, R = 2^256) for the Lagrange digits of one or two combines:
+// on the host they cost tens of microseconds, less than a kernel launch of k_interp_digits.
+struct HFr {
+  uint64_t l[4];
+};
+constexpr uint64_t HFR_P[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                               0x73eda753299d7d48ull};
+constexpr uint64_t HFR_NP = 0xfffffffeffffffffull;  // -r^-1 mod 2^64
+constexpr uint64_t HFR_R2[4] = {0xc999e990f3f29c6dull, 0x2b6cedcb87925c23ull, 0x05d314967254398full,
+                                0x0748d9d99f59ff11ull};
+using u128 = unsigned __int128;
+
+bool hfr_geq_p(const uint64_t* a) {
+  for (int i = 3; i >= 0; i--)
+    if (a[i] != HFR_P[i]) return a[i] > HFR_P[i];
+  return true;
+}
+void hfr_sub_p(uint64_t* a) {
+  u128 br = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 d = (u128)a[i] - HFR_P[i] - br;
+    a[i] = (uint64_t)d;
+    br = (d >> 64) ? 1 : 0;
+  }
+}
+HFr hfr_mul(const HFr& a, const HFr& b) {  // CIOS
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      c += (u128)a.l[j] * b.l[i] + t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[4];
+    t[4] = (uint64_t)c;
+    t[5] = (uint64_t)(c >> 64);
+    const uint64_t m = t[0] * HFR_NP;
+    c = (u128)m * HFR_P[0] + t[0];
+    c >>= 64;
+    for (int j = 1; j < 4; j++) {
+      c += (u128)m * HFR_P[j] + t[j];
+      t[j - 1] = (uint64_t)c;
+      c >>= 64;
+    }
+    c += t[4];
+    t[3] = (uint64_t)c;
+    t[4] = t[5] + (uint64_t)(c >> 64);
+  }
+  HFr r{{t[0], t[1], t[2], t[3]}};
+  if (t[4] || hfr_geq_p(r.l)) hfr_sub_p(r.l);
+  return r;
+}
+HFr hfr_from_u64(uint64_t v) { return hfr_mul(HFr{{v, 0, 0, 0}}, HFr{{HFR_R2[0], HFR_R2[1], HFR_R2[2], HFR_R2[3]}}); }
+HFr hfr_sub(const HFr& a, const HFr& b) {
+  HFr r;
+  u128 br = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 d = (u128)a.l[i] - b.l[i] - br;
+    r.l[i] = (uint64_t)d;
+    br = (d >> 64) ? 1 : 0;
+  }
+  if (br) {
+    u128 c = 0;
+    for (int i = 0; i < 4; i++) {
+      c += (u128)r.l[i] + HFR_P[i];
+      r.l[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  return r;
+}
+bool hfr_is_zero(const HFr& a) { return !(a.l[0] | a.l[1] | a.l[2] | a.l[3]); }
+HFr hfr_inv(const HFr& a) {  // a^(r-2)
+  uint64_t e[4] = {HFR_P[0] - 2, HFR_P[1], HFR_P[2], HFR_P[3]};
+  HFr r = hfr_from_u64(1);
+  for (int i = 255; i >= 0; i--) {
+    r = hfr_mul(r, r);
+    if ((e[i >> 6] >> (i & 63)) & 1) r = hfr_mul(r, a);
+  }
+  return r;
+}
+void hfr_to_canon(const HFr& a, uint64_t* out) {
+  const HFr c = hfr_mul(a, HFr{{1, 0, 0, 0}});
+  for (int i = 0; i < 4; i++) out[i] = c.l[i];
+}
+
+// k_interp_digits on the host: the four GLS digits (base |x|) of every lambda_k(0) of each combine;
+// status[c] = HBH_ERR_DUPLICATE_ENTRY and zero digits on a repeated x
+void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* digits, int* status) {
+  constexpr uint64_t XA = 0xd201000000010000ull;
+  std::vector<HFr> x(m), num(m), den(m), pre(m);
+  for (size_t c = 0; c < ncomb; c++) {
+    const uint32_t* cx = xs + c * m;
+    for (size_t k = 0; k < m; k++) x[k] = hfr_from_u64(cx[k]);
+    bool dup = false;
+    for (size_t k = 0; k < m; k++) {
+      HFr n = hfr_from_u64(1), d = hfr_from_u64(1);
+      for (size_t j = 0; j < m; j++) {
+        if (j == k) continue;
+        n = hfr_mul(n, x[j]);
+        d = hfr_mul(d, hfr_sub(x[j], x[k]));
+      }
+      dup = dup || hfr_is_zero(d);
+      num[k] = n;
+      den[k] = d;
+    }
+    status[c] = dup ? HBH_ERR_DUPLICATE_ENTRY : HBH_OK;
+    uint64_t* dg = digits + c * m * 4;
+    if (dup) {
+      std::memset(dg, 0, m * 4 * sizeof(uint64_t));
+      continue;
+    }
+    pre[0] = den[0];
+    for (size_t k = 1; k < m; k++) pre[k] = hfr_mul(pre[k - 1], den[k]);
+    HFr inv = hfr_inv(pre[m - 1]);
+    for (size_t k = m; k-- > 0;) {
+      const HFr ik = k ? hfr_mul(inv, pre[k - 1]) : inv;
+      if (k) inv = hfr_mul(inv, den[k]);
+      uint64_t q[4];
+      hfr_to_canon(hfr_mul(num[k], ik), q);
+      for (int j = 0; j < 3; j++) {  // q <- q / |x|, digit j = remainder
+        u128 rem = 0;
+        for (int w = 3; w >= 0; w--) {
+          const u128 cur = (rem << 64) | q[w];
+          q[w] = (uint64_t)(cur / XA);
+          rem = cur % XA;
+        }
+        dg[k * 4 + j] = (uint64_t)rem;
+      }
+      dg[k * 4 + 3] = q[0];
+    }
+  }
+}
+
 // G2 combines: few combines (latency-bound: the chip is idle but for the serial chains) take the
-// lane-pair form (k_interp_digits + k_interp_pair); many take k_interp_endo (throughput form).
+// lane-pair form (digits + k_interp_pair); many take k_interp_endo (throughput form).  With the x
+// values on the host and at most HOST_DIGITS_MAX combines, the digits are computed on the host and
+// uploaded (status too) instead of running k_interp_digits.
 constexpr size_t INTERP_PAIR_MAX = 64;
+constexpr size_t HOST_DIGITS_MAX = 2;
 int launch_combine_g2(hbh_engine* e, hipStream_t s, size_t ncomb, size_t m, const uint32_t* d_xs, const void* d_pts,
-                      void* d_out, int* d_status) {
+                      void* d_out, int* d_status, const uint32_t* h_xs = nullptr) {
   if (ncomb <= INTERP_PAIR_MAX && hbl::interp_g2_pair_fits((int)m)) {
     HBH_CHECK(e->in_d.ensure(ncomb * m * 4 * sizeof(uint64_t)));
-    HBH_CHECK(hbl::interp_digits(s, (int)ncomb, (int)m, d_xs, (uint64_t*)e->in_d.p, d_status));
+    if (h_xs && ncomb <= HOST_DIGITS_MAX) {
+      e->h_digits.resize(ncomb * m * 4);
+      e->h_status.resize(ncomb);
+      host_interp_digits(h_xs, ncomb, m, e->h_digits.data(), e->h_status.data());
+      HBH_CHECK(hipMemcpyAsync(e->in_d.p, e->h_digits.data(), ncomb * m * 32, hipMemcpyHostToDevice, s));
+      HBH_CHECK(hipMemcpyAsync(d_status, e->h_status.data(), ncomb * sizeof(int), hipMemcpyHostToDevice, s));
+    } else {
+      HBH_CHECK(hbl::interp_digits(s, (int)ncomb, (int)m, d_xs, (uint64_t*)e->in_d.p, d_status));
+    }
     HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)e->in_d.p, d_pts, d_out));
     return HBH_OK;
   }
@@ -579,7 +728,8 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
   HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
   if (g2) {
-    rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p);
+    rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
+                           xs.data());
     if (rc) return rc;
   } else {
     HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
@@ -655,7 +805,8 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
   HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p12.data(), p12.size(), hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p);
+  rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
+                         xs.data());
   if (rc) return rc;
   e->timer.end(s, tm);
   rc = run_pairing_dev(e, s, ncomb, e->in_p1.p, e->in_q1.p, ncomb, nullptr, nullptr, e->out_x.p, ncomb, nullptr, 1,
