@@ -177,9 +177,9 @@ HP_D bool side_init(const PairSide& s, int i, bool negate, SideState& st) {
   return true;
 }
 
-// multiply the side's line of this step into f
+// the side's line of this step, evaluated at P: (c0, c1 xP, c4 yP), or 1 for an inactive pair
 template <bool WALK, bool GEN, bool DBL>
-HP_D H12 side_line(const H12& f, const PairSide& s, SideState& st, int step, bool negate) {
+HP_D HLine side_line(const PairSide& s, SideState& st, int step, bool negate) {
   HLine l;
   if (WALK) {
     if (DBL) {
@@ -204,10 +204,11 @@ HP_D H12 side_line(const H12& f, const PairSide& s, SideState& st, int step, boo
       l.c4.l[j] = w[2 * NL + j];
     }
   }
-  const Fp c0 = st.act ? l.c0 : h_one();
-  const Fp c1 = st.act ? fp_mul(l.c1, side_xP<GEN>(st)) : fp_zero();
-  const Fp c4 = st.act ? fp_mul(l.c4, side_yP<GEN>(st, negate)) : fp_zero();
-  return h12_mul_014(f, c0, c1, c4);
+  HLine e;
+  e.c0 = st.act ? l.c0 : h_one();
+  e.c1 = st.act ? fp_mul(l.c1, side_xP<GEN>(st)) : fp_zero();
+  e.c4 = st.act ? fp_mul(l.c4, side_yP<GEN>(st, negate)) : fp_zero();
+  return e;
 }
 
 struct PairArgs {
@@ -237,13 +238,18 @@ __global__ void __launch_bounds__(256, 2) k_pair_verify(PairArgs a) {
   int step = 0;
 #pragma unroll 1
   for (int b = 62; b >= 0; b--) {
+    // the two sides' lines are multiplied together first, then into f (h12_mul_lines)
     if (b != 62) f = h12_sqr(f);
-    f = side_line<W1, G1, true>(f, a.s1, A, step, false);
-    f = side_line<W2, G2, true>(f, a.s2, B, step, neg2);
+    {
+      const HLine la = side_line<W1, G1, true>(a.s1, A, step, false);
+      const HLine lb = side_line<W2, G2, true>(a.s2, B, step, neg2);
+      f = h12_mul_lines(f, la.c0, la.c1, la.c4, lb.c0, lb.c1, lb.c4);
+    }
     step++;
     if ((hb::X_ABS >> b) & 1) {
-      f = side_line<W1, G1, false>(f, a.s1, A, step, false);
-      f = side_line<W2, G2, false>(f, a.s2, B, step, neg2);
+      const HLine la = side_line<W1, G1, false>(a.s1, A, step, false);
+      const HLine lb = side_line<W2, G2, false>(a.s2, B, step, neg2);
+      f = h12_mul_lines(f, la.c0, la.c1, la.c4, lb.c0, lb.c1, lb.c4);
       step++;
     }
   }
