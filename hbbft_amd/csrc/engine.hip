@@ -153,19 +153,24 @@ int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, 
 
 int resolve_impl(const hbh_engine* e, size_t n) {
   if (e->impl != HBH_IMPL_AUTO) return e->impl;
+  if (n <= HBH_AUTO_WAVE_MAX) return HBH_IMPL_WAVE;
   return n < HBH_AUTO_LANE_COOP_MAX ? HBH_IMPL_LANE_COOP : HBH_IMPL_PAIR;
+}
+// PAIR and WAVE share the pair_prep line tables and the two table slots of the _dev calls
+bool uses_pair_tables(int impl) { return impl == HBH_IMPL_PAIR || impl == HBH_IMPL_WAVE;
 }
 
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
 // table (k_pair_prep); every other side is walked inside the verify kernel.
-int launch_pair(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
+int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
                 const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2, int flags,
                 uint8_t* d_v, uint32_t* d_value, int slot) {
   hbl::PairSideDesc sd[2] = {{d_p1, d_q1, nullptr, nullptr, d_i1, nq1}, {d_p2, d_q2, nullptr, nullptr, d_i2, nq2}};
   DevBuf* tab[2] = {&e->ptab[slot][0], &e->ptab[slot][1]};
   DevBuf* inf[2] = {&e->pinf[slot][0], &e->pinf[slot][1]};
   for (int k = 0; k < 2; k++) {
-    if (!sd[k].idx || sd[k].nq * 4 > n) continue;
+    // WAVE walks every side: a table costs a serial 68-step walk (k_pair_prep) before the first check
+    if (!sd[k].idx || sd[k].nq * 4 > n || impl == HBH_IMPL_WAVE) continue;
     HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
     HBH_CHECK(inf[k]->ensure(sd[k].nq));
     hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
@@ -175,7 +180,10 @@ int launch_pair(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const 
     sd[k].qinf = (const uint8_t*)inf[k]->p;
   }
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  if (impl == HBH_IMPL_WAVE)
+    HBH_CHECK(hbl::wave_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  else
+    HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   e->timer.end(s, t);
   return HBH_OK;
 }
@@ -210,8 +218,8 @@ int run_pairing_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, co
   if (n == 0) return HBH_OK;
   if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
   const int impl = resolve_impl(e, n);
-  if (impl == HBH_IMPL_PAIR)
-    return launch_pair(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value, slot);
+  if (uses_pair_tables(impl))
+    return launch_pair(e, s, impl, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value, slot);
   if (!d_p1 || !d_p2) {
     const void* g = nullptr;
     int rc = g1_repeated(e, s, n, &g);
@@ -382,7 +390,7 @@ int hbh_verify_pairing_eq_dev(hbh_engine* e, void* stream, size_t n, const void*
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  if (n && resolve_impl(e, n) == HBH_IMPL_PAIR) {
+  if (n && uses_pair_tables(resolve_impl(e, n))) {
     // table slot of its own: wait for the last general call and for this slot's previous user only
     const int slot = e->slot;
     e->slot ^= 1;
@@ -457,7 +465,8 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
-  if (impl != HBH_IMPL_LANE_COOP && impl != HBH_IMPL_THREAD_SIGNED && impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO)
+  if (impl != HBH_IMPL_LANE_COOP && impl != HBH_IMPL_THREAD_SIGNED && impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO &&
+      impl != HBH_IMPL_WAVE)
     return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;

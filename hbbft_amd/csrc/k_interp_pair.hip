@@ -111,19 +111,6 @@ HP_D HJac hj_mul_affine(const Fp& x, const Fp& y, bool inf, uint32_t k) {
 HP_D Fp psi_xh(const Fp& x) { return fp_reduce(fp_mul(dpp_fp<DPP_SWAP>(x), fp_const(hb::PSI_C1_C1))); }
 HP_D Fp psi_yh(const Fp& y) { return fp_reduce(h_mul(h_conj(y), h_const(hb::PSI_C2_C0, hb::PSI_C2_C1))); }
 
-// 1 / a in Fp2 with a variable-time inverse of the (public) norm: both lanes invert the same norm
-HP_D Fp h_inv_vartime(const Fp& a) {
-  const Fp s = fp_sqr(a);
-  const Fp n = fp_add(s, dpp_fp<DPP_SWAP>(s));
-  uint32_t w[12], p[12], r[12];
-  fp_to_words(n, w);
-#pragma unroll
-  for (int i = 0; i < 12; i++) p[i] = hb::PM2_W[i];
-  p[0] += 2;  // p - 2 + 2
-  hb::words_inv_vartime<12>(w, p, r);
-  return h_conj(fp_mul(a, fp_from_words(r)));
-}
-
 HP_D void lds_put(uint32_t* s, const HJac& p) {
 #pragma unroll
   for (int i = 0; i < NL; i++) {

@@ -1,0 +1,423 @@
+// HBH_IMPL_WAVE: one WAVE per pairing check -- the latency kernel (gfx950).
+//
+// The lane-pair kernel (k_pair.hip) gives a check two lanes and runs its ~5,400 Fp2 products one
+// after another; that is the right shape for 65,536 checks and the wrong one for the master check
+// of combine_and_verify_sig (src/threshold_sign.rs:264) or the small per-message batches of the
+// protocol flows, where one check's serial chain is the whole latency.  Here a check owns a wave:
+// 32 lane pairs, each computing one Fp2 product (pfp.hpp lane-pair split: even lane c0, odd lane
+// c1), so every Fp12 / curve operation of a step runs as ~20 independent products side by side.
+//
+// The kernel is an interpreter of the stage programs built by tools/gen_wave_prog.py
+// (wave_prog.inc): the check's state lives in LDS slots (one Fp2 = 2 x 16 words, stride 36 words);
+// each stage is a product phase (pair j: X = +-(S[a] +- S[b]), Y = +-(S[c] +- S[d]);
+// PROD_j = X*Y | X1*Y1 + X2*Y2 | X^2) and an assembly phase (pair o: S[dst_o] = sum c V + xi sum
+// c' V', reduced, optionally replaced by 1 / 0 when its pair is inactive), separated by barriers.
+// The programs are the formulas of k_pair.hip (pairing 0.14 lines, final_exp_x3 chain); their
+// exact emulation is checked against the oracle on the CPU (tests/test_wave_prog.py).
+//
+// One 64-thread workgroup per check; 190 slots = 27 KiB of LDS per check.
+#include "launch.hpp"
+#include "pfp.hpp"
+#include "wave_prog.inc"
+
+namespace hbs {
+
+constexpr int WV_STRIDE = 36;  // words per slot (2 components x 16, +4 against bank conflicts)
+constexpr int WV_LINE_Q4 = 11;  // k_pair_prep table: 16-byte chunks per (line, lane component)
+constexpr uint32_t WV_ZW[NL] = {0};
+
+struct WaveSide {
+  const uint32_t* p;    // G1 points (24 words), nullptr = the generator
+  const uint32_t* q;    // WALK: G2 points (48 words)
+  const int4* lines;    // TABLE: k_pair_prep line tables (nullptr = WALK)
+  const uint8_t* qinf;  // TABLE: 1 = table point at infinity
+  const uint32_t* idx;  // Q index per check (nullptr = identity)
+  uint32_t nq;
+};
+
+struct WaveArgs {
+  int n;
+  WaveSide s[2];
+  int flags;            // bit 0: negate P2; bit 1: conjugated value (single pairing)
+  uint8_t* verdict;
+  uint32_t* value_out;  // 144 canonical words per check (may be null)
+};
+
+// ---------------------------------------------------------------- LDS slots
+HP_D Fp ld_own(const uint32_t* sm, int slot, int h) {
+  const int4* p = (const int4*)(sm + slot * WV_STRIDE + h * 16);
+  Fp r;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int4 v = p[q];
+    r.l[4 * q] = v.x;
+    r.l[4 * q + 1] = v.y;
+    if (4 * q + 2 < NL) r.l[4 * q + 2] = v.z;
+    if (4 * q + 3 < NL) r.l[4 * q + 3] = v.w;
+  }
+  return r;
+}
+HP_D void st_own(uint32_t* sm, int slot, int h, const Fp& a) {
+  int4* p = (int4*)(sm + slot * WV_STRIDE + h * 16);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int i = 4 * q;
+    p[q] = make_int4(a.l[i], a.l[i + 1], i + 2 < NL ? a.l[i + 2] : 0, i + 3 < NL ? a.l[i + 3] : 0);
+  }
+}
+
+// X = sgn * (S[a] + s * S[b]); s in {0, 1, -1} (codes 0, 1, 2), sgn = -1 for neg, -1 on the odd
+// lane for conj.  Lazy limbs (|limb| < 2^29); normalised when `norm`.
+HP_D Fp operand(const uint32_t* sm, int h, int a, int b, int scode, int negb, int conjb, bool sum, bool sgnflag,
+                bool norm) {
+  Fp x = ld_own(sm, a, h);
+  if (sum) {
+    const Fp y = ld_own(sm, b, h);
+    const int32_t z = scode ? -1 : 0;
+    const int32_t m = scode == 2 ? -1 : 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) x.l[i] += ((y.l[i] ^ m) - m) & z;
+  }
+  if (sgnflag) {
+    const int32_t m = (negb ^ (conjb & h)) ? -1 : 0;
+#pragma unroll
+    for (int i = 0; i < NL; i++) x.l[i] = (x.l[i] ^ m) - m;
+  }
+  if (norm) fp_norm(x);
+  return x;
+}
+
+// own component of sum_t x_t * y_t (Fp2, lane-pair split of pfp.hpp h_mul_l), one reduction
+template <int K>
+HP_D Fp wv_mul(const Fp (&x)[K], const Fp (&y)[K]) {
+  const int32_t sm = lp_even() ? -1 : 0;
+  int32_t Y[K][NL], W[K][NL], Z[K][NL];
+#pragma unroll
+  for (int t = 0; t < K; t++)
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+      Y[t][i] = dpp<DPP_EVEN>(y[t].l[i]);
+      W[t][i] = dpp<DPP_ODD>(y[t].l[i]);
+      Z[t][i] = (dpp<DPP_SWAP>(x[t].l[i]) ^ sm) - sm;
+    }
+  int32_t m[NL];
+  int64_t acc = 0;
+  Fp r;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int t = 0; t < K; t++)
+#pragma unroll
+      for (int i = 0; i <= k; i++) {
+        acc += (int64_t)x[t].l[i] * Y[t][k - i];
+        acc += (int64_t)Z[t][i] * W[t][k - i];
+      }
+#pragma unroll
+    for (int i = 0; i < k; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+    m[k] = (int32_t)(((uint32_t)acc * NP0) & (uint32_t)MASK28);
+    acc += (int64_t)m[k] * (int32_t)P_L[0];
+    acc >>= 28;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int t = 0; t < K; t++)
+#pragma unroll
+      for (int i = k - NL + 1; i < NL; i++) {
+        acc += (int64_t)x[t].l[i] * Y[t][k - i];
+        acc += (int64_t)Z[t][i] * W[t][k - i];
+      }
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+    r.l[k - NL] = (int32_t)acc & MASK28;
+    acc >>= 28;
+  }
+  r.l[NL - 1] = (int32_t)acc;
+  return r;
+}
+
+template <int K>
+HP_D Fp product(const uint32_t* sm, int h, const uint64_t* d, uint32_t fl) {
+  const bool xs = fl & 0x100, ys = fl & 0x200, sg = fl & 0xC00;
+  Fp x[K], y[K];
+#pragma unroll
+  for (int t = 0; t < K; t++) {
+    const uint64_t w = d[t];
+    const int hi = (int)(w >> 32);
+    x[t] = operand(sm, h, (int)(w & 0xFF), (int)((w >> 8) & 0xFF), hi & 3, (hi >> 4) & 1, (hi >> 5) & 1, xs, sg, false);
+    y[t] = operand(sm, h, (int)((w >> 16) & 0xFF), (int)((w >> 24) & 0xFF), (hi >> 2) & 3, (hi >> 6) & 1,
+                   (hi >> 7) & 1, ys, sg, ys || sg);
+  }
+  return wv_mul<K>(x, y);
+}
+
+HP_D Fp product_sq(const uint32_t* sm, int h, uint64_t w, uint32_t fl) {
+  const int hi = (int)(w >> 32);
+  const bool xs = fl & 0x100, sg = fl & 0xC00;
+  const Fp x = operand(sm, h, (int)(w & 0xFF), (int)((w >> 8) & 0xFF), hi & 3, (hi >> 4) & 1, (hi >> 5) & 1, xs, sg,
+                       xs || sg);
+  return h_sqr(x);
+}
+
+// dst = sum c V + xi sum c' V' (8 x u16 descriptor: dst | gate << 8 | defone << 10, then terms
+// src | coef (4-bit signed) << 8 | conj << 12), reduced; gated outputs of an inactive pair take 1 / 0
+HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, bool act1) {
+  const uint16_t ws[8] = {(uint16_t)dw.x, (uint16_t)(dw.x >> 16), (uint16_t)dw.y, (uint16_t)(dw.y >> 16),
+                          (uint16_t)dw.z, (uint16_t)(dw.z >> 16), (uint16_t)dw.w, (uint16_t)(dw.w >> 16)};
+  int32_t ap[NL], at[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    ap[i] = 0;
+    at[i] = 0;
+  }
+#pragma unroll
+  for (int t = 0; t < 7; t++) {
+    if (t < j1 + j2) {  // uniform across the wave
+      const int tm = ws[1 + t];
+      int c = (tm >> 8) & 0xF;
+      c = c >= 8 ? c - 16 : c;
+      if ((tm >> 12) & h & 1) c = -c;
+      const Fp v = ld_own(sm, tm & 0xFF, h);
+      if (t < j1) {
+#pragma unroll
+        for (int i = 0; i < NL; i++) ap[i] += c * v.l[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < NL; i++) at[i] += c * v.l[i];
+      }
+    }
+  }
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = ap[i];
+  if (j2) {
+    Fp t;
+#pragma unroll
+    for (int i = 0; i < NL; i++) t.l[i] = at[i];
+    fp_norm(r);
+    fp_norm(t);
+    const Fp pt = dpp_fp<DPP_SWAP>(t);
+    // xi (t0 + t1 u) = (t0 - t1) + (t0 + t1) u
+#pragma unroll
+    for (int i = 0; i < NL; i++) r.l[i] += t.l[i] + (h ? pt.l[i] : -pt.l[i]);
+  }
+  fp_norm(r);
+  r = fp_reduce(r);
+  const int gate = (ws[0] >> 8) & 3;
+  if ((gate == 1 && !act0) || (gate == 2 && !act1)) r = ((ws[0] >> 10) & 1) ? h_one() : h_zero();
+  st_own(sm, ws[0] & 0xFF, h, r);
+}
+
+HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0, bool act1, const int4* tl0,
+                     const int4* tl1) {
+  const uint4* hdr = (const uint4*)hbw::WP_HDR;
+#pragma unroll 1
+  for (int st = off; st < off + nst; st++) {
+    const uint4 hd = hdr[st];
+    const uint32_t fl = hd.x;
+    const int kind = fl & 3, j1 = (fl >> 2) & 7, j2 = (fl >> 5) & 7, special = (fl >> 12) & 0xF;
+    const int npairs = (fl >> 16) & 63, nouts = (fl >> 22) & 63;
+    // table lines requested by this stage, fetched now and written after the assembly phase
+    int4 tline[WV_LINE_Q4];
+    int tslot = -1;
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+      const uint32_t e = (hd.w >> (16 * side)) & 0xFFFF;
+      if (special == 0 && (e & 1) && pair == side) {
+        const int4* src = (side ? tl1 : tl0) + ((size_t)((e >> 1) & 0x7F) * 2 + h) * WV_LINE_Q4;
+#pragma unroll
+        for (int k = 0; k < WV_LINE_Q4; k++) tline[k] = src[k];
+        tslot = (int)(e >> 8);
+      }
+    }
+    if (special == 1) {
+      if (pair == 0) {
+        const Fp v = ld_own(sm, hd.w & 0xFF, h);
+        st_own(sm, (hd.w >> 8) & 0xFF, h, fp_reduce(h_inv_vartime(v)));
+      }
+    } else if (kind != 3 && pair < npairs) {
+      Fp r;
+      if (kind == 1) {
+        const uint64_t* d = hbw::WP_PDESC + hd.y + 2 * pair;
+        const uint64_t dd[2] = {d[0], d[1]};
+        r = product<2>(sm, h, dd, fl);
+      } else if (kind == 2) {
+        r = product_sq(sm, h, hbw::WP_PDESC[hd.y + pair], fl);
+      } else {
+        const uint64_t dd[1] = {hbw::WP_PDESC[hd.y + pair]};
+        r = product<1>(sm, h, dd, fl);
+      }
+      st_own(sm, hbw::WP_PROD + pair, h, r);
+    }
+    __syncthreads();
+    if (pair < nouts) {
+      const uint4 dw = ((const uint4*)hbw::WP_ADESC)[hd.z + pair];
+      assemble(sm, h, dw, j1, j2, act0, act1);
+    }
+    if (tslot >= 0) {
+      int32_t w[4 * WV_LINE_Q4];
+#pragma unroll
+      for (int k = 0; k < WV_LINE_Q4; k++) {
+        w[4 * k] = tline[k].x;
+        w[4 * k + 1] = tline[k].y;
+        w[4 * k + 2] = tline[k].z;
+        w[4 * k + 3] = tline[k].w;
+      }
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        Fp v;
+#pragma unroll
+        for (int i = 0; i < NL; i++) v.l[i] = w[c * NL + i];
+        st_own(sm, tslot + c, h, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// constant slots (tools/gen_wave_prog.py CONSTS): pair k writes slot k
+HP_D void put_const(uint32_t* sm, int h, int slot, const uint32_t (&c0)[NL], const uint32_t (&c1)[NL]) {
+  Fp v;
+#pragma unroll
+  for (int i = 0; i < NL; i++) v.l[i] = (int32_t)(h ? c1[i] : c0[i]);
+  st_own(sm, slot, h, v);
+}
+
+// side K of check i: writes its slots (pair K: XP, YP; pair 2 + K: QX, QY, T), returns the line
+// table of a TABLE side; bad = Q index out of range
+template <int K>
+HP_D const int4* wave_side(const WaveArgs& a, uint32_t* sm, int i, int h, int pair, bool& act, bool& bad) {
+  const WaveSide& s = a.s[K];
+  const uint32_t q = s.idx ? s.idx[i] : (uint32_t)i;
+  act = false;
+  bad = q >= s.nq;
+  if (bad) return nullptr;
+  const bool neg = K == 1 && (a.flags & 1);
+  bool pinf = false;
+  Fp xp, yp;
+  if (s.p) {
+    const uint32_t* w = s.p + (size_t)i * 24;
+    pinf = words_zero(w, 24);
+    xp = fp_from_words(w);
+    yp = fp_from_words(w + 12);
+    if (neg) yp = fp_neg(yp);
+  } else {
+    xp = fp_const(hb::G1X_M);
+    yp = fp_const(neg ? hb::G1NY_M : hb::G1Y_M);
+  }
+  const int base = K ? hbw::WP_SIDE1 : hbw::WP_SIDE0;
+  const int4* tl = nullptr;
+  bool qinf;
+  if (s.lines) {
+    qinf = s.qinf[q] != 0;
+    tl = s.lines + (size_t)q * 68 * 2 * WV_LINE_Q4;
+  } else {
+    const uint32_t* w = s.q + (size_t)q * 48;
+    qinf = words_zero(w, 48);
+    if (pair == 2 + K) {
+      Fp xq, yq;
+      h_g2_load(w, xq, yq);
+      if (qinf) {
+        xq = h_one();
+        yq = h_one();
+      }
+      st_own(sm, base + 2, h, xq);
+      st_own(sm, base + 3, h, yq);
+      st_own(sm, base + 4, h, xq);
+      st_own(sm, base + 5, h, yq);
+      st_own(sm, base + 6, h, h_one());
+    }
+  }
+  if (pair == K) {
+    st_own(sm, base + 0, h, h ? fp_zero() : xp);
+    st_own(sm, base + 1, h, h ? fp_zero() : yp);
+  }
+  act = !pinf && !qinf;
+  return tl;
+}
+
+__global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
+  extern __shared__ uint32_t sm[];
+  const int i = blockIdx.x;
+  if (i >= a.n) return;
+  const int lane = threadIdx.x, h = lane & 1, pair = lane >> 1;
+  switch (pair) {
+    case 0: put_const(sm, h, 0, WV_ZW, WV_ZW); break;
+    case 1: put_const(sm, h, 1, hb::ONE_L, WV_ZW); break;
+    case 2: put_const(sm, h, 2, hb::FROB1_0_C0, hb::FROB1_0_C1); break;
+    case 3: put_const(sm, h, 3, hb::FROB1_1_C0, hb::FROB1_1_C1); break;
+    case 4: put_const(sm, h, 4, hb::FROB1_2_C0, hb::FROB1_2_C1); break;
+    case 5: put_const(sm, h, 5, hb::FROB1_3_C0, hb::FROB1_3_C1); break;
+    case 6: put_const(sm, h, 6, hb::FROB1_4_C0, hb::FROB1_4_C1); break;
+    case 7: put_const(sm, h, 7, hb::FROB1_5_C0, hb::FROB1_5_C1); break;
+    case 8: put_const(sm, h, 8, hb::FROB2_0_C0, WV_ZW); break;
+    case 9: put_const(sm, h, 9, hb::FROB2_1_C0, WV_ZW); break;
+    case 10: put_const(sm, h, 10, hb::FROB2_2_C0, WV_ZW); break;
+    case 11: put_const(sm, h, 11, hb::FROB2_3_C0, WV_ZW); break;
+    case 12: put_const(sm, h, 12, hb::FROB2_4_C0, WV_ZW); break;
+    case 13: put_const(sm, h, 13, hb::FROB2_5_C0, WV_ZW); break;
+    case 14: put_const(sm, h, 14, hb::G1X_M, WV_ZW); break;
+    case 15: put_const(sm, h, 15, hb::G1Y_M, WV_ZW); break;
+    case 16: put_const(sm, h, 16, hb::G1NY_M, WV_ZW); break;
+    case 17: put_const(sm, h, hbw::WP_F, hb::ONE_L, WV_ZW); break;
+    default:
+      if (pair < 23) put_const(sm, h, hbw::WP_F + pair - 17, WV_ZW, WV_ZW);
+      break;
+  }
+  // the two sides: P (G1) -> XP, YP as Fp2 (x, 0); Q -> QX, QY and T = (Q, 1); activity flags
+  bool act0, act1, bad0, bad1;
+  const int4* tl0 = wave_side<0>(a, sm, i, h, pair, act0, bad0);
+  const int4* tl1 = wave_side<1>(a, sm, i, h, pair, act1, bad1);
+  const bool bad = bad0 || bad1;
+  if (bad) {  // index out of range: reject, never read past a table (uniform per workgroup)
+    if (lane == 0 && a.verdict) a.verdict[i] = 0;
+    return;
+  }
+  __syncthreads();
+  const int mv = (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
+  run_stages(sm, hbw::WP_MILLER_OFF[mv], hbw::WP_MILLER_N[mv], h, pair, act0, act1, tl0, tl1);
+  run_stages(sm, hbw::WP_FE_OFF, hbw::WP_FE_N, h, pair, act0, act1, tl0, tl1);
+  // e = f^(3 (p^12 - 1) / r) in slots E0..E5 (w-basis)
+  bool ok = true;
+  if (pair < 6) {
+    Fp v = ld_own(sm, hbw::WP_E + pair, h);
+    if (a.value_out) {
+      if ((a.flags & 2) && (pair & 1)) v = fp_neg(v);
+      const int pos = (pair & 1) ? 3 + (pair >> 1) : (pair >> 1);
+      fp_to_words(v, a.value_out + (size_t)i * 144 + 24 * pos + 12 * h);
+    }
+    const Fp want = (pair == 0) ? h_one() : h_zero();
+    ok = fp_is_zero(fp_sub(v, want));
+  }
+  const bool all = __all(ok);
+  if (lane == 0 && a.verdict) a.verdict[i] = all ? 1 : 0;
+}
+
+}  // namespace hbs
+
+namespace hbl {
+
+size_t wave_lds_bytes() { return (size_t)hbw::WP_NSLOTS * hbs::WV_STRIDE * 4; }
+
+hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
+                       uint8_t* verdict, uint32_t* value_out) {
+  if (n <= 0) return hipSuccess;
+  hbs::WaveArgs a;
+  a.n = n;
+  const PairSideDesc* d[2] = {&d1, &d2};
+  for (int k = 0; k < 2; k++) {
+    a.s[k].p = (const uint32_t*)d[k]->p;
+    a.s[k].q = (const uint32_t*)d[k]->q;
+    a.s[k].lines = (const int4*)d[k]->lines;
+    a.s[k].qinf = d[k]->qinf;
+    a.s[k].idx = d[k]->idx;
+    a.s[k].nq = (uint32_t)d[k]->nq;
+  }
+  a.flags = flags;
+  a.verdict = verdict;
+  a.value_out = value_out;
+  hipLaunchKernelGGL(hbs::k_wave, dim3((unsigned)n), dim3(64), wave_lds_bytes(), s, a);
+  return hipGetLastError();
+}
+
+}  // namespace hbl

@@ -62,6 +62,14 @@ hipError_t pair_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* 
 hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
                        uint8_t* verdict, uint32_t* value_out);
 
+// --------------------------------------------------------------- wave-per-check pairing (k_wave.hip)
+// The same verdicts / values as pair_verify with one 64-lane workgroup per check (the latency
+// kernel: a check's Fp2 products run on 32 lane pairs side by side).  TABLE sides read pair_prep
+// tables; wave_lds_bytes() of LDS per workgroup.
+size_t wave_lds_bytes();
+hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
+                       uint8_t* verdict, uint32_t* value_out);
+
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).
 hipError_t g1_mul(hipStream_t s, int n, const void* pts, const uint32_t* scalars, void* out);

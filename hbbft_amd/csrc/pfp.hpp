@@ -24,6 +24,7 @@
 //   Fp12 values between operations are reduced (|.| < 2p), as in stower.hpp whose formulas these are.
 #pragma once
 #include "sfp.hpp"
+#include "words.hpp"
 
 #define HP_D __device__ __forceinline__
 
@@ -140,6 +141,24 @@ HP_D Fp h_inv(const Fp& a) {
   const Fp n = fp_reduce(fp_add(s, dpp_fp<DPP_SWAP>(s)));
   const Fp t = fp_inv(n);
   return h_conj(fp_mul(a, t));
+}
+
+// 1 / a in Fp2 with a variable-time inverse of the (public) norm: both lanes invert the same norm.
+// a = 0 gives 0 (the binary Euclid loop would not terminate on a zero norm).
+HP_D Fp h_inv_vartime(const Fp& a) {
+  const Fp s = fp_sqr(a);
+  const Fp n = fp_add(s, dpp_fp<DPP_SWAP>(s));
+  uint32_t w[12], p[12], r[12];
+  fp_to_words(n, w);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) nz |= w[i];
+  if (nz == 0) return fp_zero();
+#pragma unroll
+  for (int i = 0; i < 12; i++) p[i] = hb::PM2_W[i];
+  p[0] += 2;  // p - 2 + 2
+  hb::words_inv_vartime<12>(w, p, r);
+  return h_conj(fp_mul(a, fp_from_words(r)));
 }
 
 // ---------------------------------------------------------------- Fp6 / Fp12 (own components)

@@ -292,7 +292,8 @@ class Engine:
 
     def set_pairing_impl(self, impl):
         """HBH_IMPL_*: 1 = lane-cooperative (six lanes per check), 2 = one thread per check (signed
-        limbs, stage kernels), 3 = auto (default), 4 = lane pair (two lanes per check, fused)."""
+        limbs, stage kernels), 3 = auto (default), 4 = lane pair (two lanes per check, fused), 5 = wave
+        (one 64-lane wave per check: the latency kernel)."""
         check(self._l.hbh_engine_set_pairing_impl(self._h, int(impl)))
 
     # ------------------------------------------------------------ profiling

@@ -273,8 +273,10 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
  *     accumulator per lane; lowest latency for small batches.
  *   HBH_IMPL_THREAD_SIGNED (k_ts_*.hip): one thread per check, stage kernels (round-1 path, kept
  *     as a cross-check).
- *   HBH_IMPL_AUTO (the default): LANE_COOP below HBH_AUTO_LANE_COOP_MAX checks per call, PAIR from
- *     there on.
+ *   HBH_IMPL_WAVE (k_wave.hip): one 64-lane wave per check; the check's Fp2 products run on 32 lane
+ *     pairs side by side.  Latency path (one check: the master check of combine_and_verify_sig).
+ *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, LANE_COOP below
+ *     HBH_AUTO_LANE_COOP_MAX, PAIR from there on.
  * HBH_IMPL_THREAD (0, the round-1 unsigned one-thread kernel) is retired: selecting it returns
  * HBH_ERR_ARG. */
 #define HBH_IMPL_THREAD 0
@@ -282,6 +284,8 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_THREAD_SIGNED 2
 #define HBH_IMPL_AUTO 3
 #define HBH_IMPL_PAIR 4
+#define HBH_IMPL_WAVE 5
+#define HBH_AUTO_WAVE_MAX 2048
 #define HBH_AUTO_LANE_COOP_MAX 16384
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 

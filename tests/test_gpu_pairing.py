@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[1, 2, 4, 3], ids=["lane_coop", "thread_signed", "pair", "auto"])
+@pytest.fixture(params=[1, 2, 4, 5, 3], ids=["lane_coop", "thread_signed", "pair", "wave", "auto"])
 def eng(engine, request):
-    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_PAIR and
-    the default HBH_IMPL_AUTO) must give identical results."""
+    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_PAIR,
+    HBH_IMPL_WAVE and the default HBH_IMPL_AUTO) must give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine
     engine.set_pairing_impl(3)
@@ -125,9 +125,12 @@ def test_implementations_agree_random_batch(engine):
     v2 = engine.verify_sig_shares(P, S, hs, D)
     engine.set_pairing_impl(4)
     v0 = engine.verify_sig_shares(P, S, hs, D)
+    engine.set_pairing_impl(5)
+    v5 = engine.verify_sig_shares(P, S, hs, D)
     engine.set_pairing_impl(3)
     assert v1 == v0
     assert v2 == v0
+    assert v5 == v0
     for i, w in want:
         assert v1[i] == int(w), i
     assert sum(v1) == sum(1 for i in range(n) if i % 11 not in (3, 5))

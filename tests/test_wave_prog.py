@@ -1,0 +1,90 @@
+"""The stage programs of the wave-per-check pairing kernel (k_wave.hip), executed by the exact
+emulator of tools/gen_wave_prog.py, against the oracle's pairing (oracle/bls12_381.py).
+
+This pins the programs -- formulas, scheduling, slot reuse, gating of inactive pairs and the
+table-line plumbing -- without a GPU; tests/test_gpu_wave.py then checks the kernel that runs them.
+"""
+import os
+import random
+import sys
+
+import pytest
+
+from oracle import bls12_381 as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import gen_wave_prog as W  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def progs():
+    return W.build()
+
+
+def wbasis(f12):
+    (c0, c1) = f12
+    out = []
+    for i in range(3):
+        out.append(tuple(x % C.P for x in c0[i]))
+        out.append(tuple(x % C.P for x in c1[i]))
+    return [out[0], out[1], out[2], out[3], out[4], out[5]]
+
+
+def tower_to_w(f12):
+    c0, c1 = f12
+    return [tuple(v % C.P for v in c0[0]), tuple(v % C.P for v in c1[0]), tuple(v % C.P for v in c0[1]),
+            tuple(v % C.P for v in c1[1]), tuple(v % C.P for v in c0[2]), tuple(v % C.P for v in c1[2])]
+
+
+def cube(f):
+    return C.f12_mul(C.f12_mul(f, f), f)
+
+
+ONE_W = [(1, 0)] + [(0, 0)] * 5
+
+
+def test_committed_include_is_current(progs, tmp_path):
+    p = tmp_path / "wave_prog.inc"
+    W.emit(progs, str(p))
+    with open(os.path.join(ROOT, "hbbft_amd", "csrc", "wave_prog.inc")) as f:
+        assert f.read() == p.read_text(), "regenerate with python tools/gen_wave_prog.py"
+
+
+def test_program_shape(progs):
+    for m, v in progs["variants"].items():
+        assert v["nstages_miller"] <= 215 and v["nstages_fe"] <= 360, m
+        assert len(progs["slots"]) <= 256
+
+
+@pytest.mark.parametrize("mode", W.MODES)
+def test_single_pairing_value(progs, mode):
+    rnd = random.Random(7 + W.MODES.index(mode))
+    Pp = C.g1_mul(C.G1_GEN, rnd.randrange(1, C.R))
+    Q = C.g2_mul(C.G2_GEN, rnd.randrange(1, C.R))
+    got = W.emulate(progs["variants"][mode], [(Pp, Q, False), (None, Q, False)], conj=True)
+    assert got == tower_to_w(cube(C.pairing(Pp, Q)))
+
+
+@pytest.mark.parametrize("mode", W.MODES)
+def test_pairing_equality(progs, mode):
+    rnd = random.Random(11 + W.MODES.index(mode))
+    a, b = rnd.randrange(1, C.R), rnd.randrange(1, C.R)
+    # e(a g1, b g2) == e(g1, ab g2): the verifier's product with P2 negated is 1
+    P1, Q1 = C.g1_mul(C.G1_GEN, a), C.g2_mul(C.G2_GEN, b)
+    Q2 = C.g2_mul(C.G2_GEN, a * b % C.R)
+    v = progs["variants"][mode]
+    assert W.emulate(v, [(P1, Q1, False), ("GEN", Q2, True)]) == ONE_W
+    Q2bad = C.g2_mul(C.G2_GEN, (a * b + 1) % C.R)
+    assert W.emulate(v, [(P1, Q1, False), ("GEN", Q2bad, True)]) != ONE_W
+
+
+def test_inactive_pairs(progs):
+    rnd = random.Random(3)
+    Pp = C.g1_mul(C.G1_GEN, rnd.randrange(1, C.R))
+    Q = C.g2_mul(C.G2_GEN, rnd.randrange(1, C.R))
+    v = progs["variants"]["WT"]
+    # both pairs at infinity -> the value is 1; one pair inactive -> the other pair's value
+    assert W.emulate(v, [(None, Q, False), (Pp, None, False)]) == ONE_W
+    got = W.emulate(v, [(None, Q, False), (Pp, Q, False)], conj=True)
+    assert got == tower_to_w(cube(C.pairing(Pp, Q)))
