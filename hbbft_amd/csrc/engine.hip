@@ -104,7 +104,7 @@ struct hbh_engine {
   std::vector<uint64_t> h_digits;
   std::vector<int> h_status;
   // workspaces
-  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep, fbtab;
+  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep, fbtab, ipart;
   bool fbtab_ready = false;  // fixed-base comb table of g1 (built on first use)
   size_t g1rep_n = 0;
   // staging for host-pointer entry points
@@ -359,7 +359,7 @@ int hbh_engine_destroy(hbh_engine* e) {
   (void)hipStreamSynchronize(e->stream);
   e->timer.clear();
   for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->lc0, &e->lc1, &e->lc2, &e->lc3,
-                    &e->g1rep, &e->fbtab, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
+                    &e->g1rep, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
                     &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1]})
     b->release();
@@ -699,7 +699,8 @@ int launch_combine_g2(hbh_engine* e, hipStream_t s, size_t ncomb, size_t m, cons
     } else {
       HBH_CHECK(hbl::interp_digits(s, (int)ncomb, (int)m, d_xs, (uint64_t*)e->in_d.p, d_status));
     }
-    HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)e->in_d.p, d_pts, d_out));
+    HBH_CHECK(e->ipart.ensure(hbl::interp_g2_pair_part_bytes((int)ncomb)));
+    HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)e->in_d.p, d_pts, e->ipart.p, d_out));
     return HBH_OK;
   }
   HBH_CHECK(hbl::combine_g2(s, (int)ncomb, (int)m, d_xs, d_pts, d_out, d_status));

@@ -16,10 +16,9 @@
 
 namespace hbs {
 
-constexpr int IP_THREADS = 512;          // 256 lane pairs per combine
+constexpr int IP_THREADS = 256;          // one workgroup per (combine, chunk): 128 lane pairs
 constexpr int IP_NCHUNK = 2;             // 32-bit chunks of the 64-bit digits
-constexpr int IP_PAIRS = IP_THREADS / 2;
-constexpr int IP_G = IP_PAIRS / IP_NCHUNK;  // lane pairs per chunk (power of two)
+constexpr int IP_G = IP_THREADS / 2;     // lane pairs per chunk (power of two)
 constexpr int IP_WORDS = 3 * NL;         // one lane's Jacobian point (x, y, z own components)
 
 HP_D bool hj_is_zero(const HJac& p) { return h_is_zero(p.z); }
@@ -130,12 +129,15 @@ HP_D HJac lds_get(const uint32_t* s) {
   return p;
 }
 
+// Workgroup (c, chunk): the chunk's terms on 128 lane pairs (4 waves, one per SIMD, so each pair's
+// serial chain has its SIMD to itself), an LDS tree, then pair 0 scales chunk 1 by 2^32 (Horner) and
+// writes its partial sum; k_interp_join adds the two partials and converts to affine.
 __global__ void __launch_bounds__(IP_THREADS) k_interp_pair(int ncomb, int m, const uint64_t* __restrict__ digits,
-                                                            const uint32_t* __restrict__ pts, uint32_t* __restrict__ out) {
+                                                            const uint32_t* __restrict__ pts, int32_t* __restrict__ part) {
   extern __shared__ uint32_t sm[];  // IP_THREADS x IP_WORDS, lane-major
-  const int c = blockIdx.x;
+  const int c = blockIdx.x / IP_NCHUNK, chunk = blockIdx.x % IP_NCHUNK;
   if (c >= ncomb) return;  // uniform per workgroup
-  const int pair = threadIdx.x >> 1, chunk = pair / IP_G, g = pair % IP_G;
+  const int g = threadIdx.x >> 1;
   HJac acc = hj_zero();
   for (int t = g; t < m * 4; t += IP_G) {
     const int k = t >> 2, j = t & 3;
@@ -162,12 +164,24 @@ __global__ void __launch_bounds__(IP_THREADS) k_interp_pair(int ncomb, int m, co
     }
     __syncthreads();
   }
-  if (pair != 0) return;
-  // R = 2^32 S_1 + S_0
-  HJac r = lds_get(sm + (size_t)(IP_G * 2 + (threadIdx.x & 1)) * IP_WORDS);
+  if (g != 0) return;
+  HJac r = lds_get(sm + (size_t)(threadIdx.x & 1) * IP_WORDS);
+  if (chunk == 1) {
 #pragma unroll 1
-  for (int b = 0; b < 32; b++) r = hj_dbl(r);
-  r = hj_add(r, lds_get(sm + (size_t)(threadIdx.x & 1) * IP_WORDS));
+    for (int b = 0; b < 32; b++) r = hj_dbl(r);
+  }
+  lds_put((uint32_t*)part + ((size_t)blockIdx.x * 2 + (threadIdx.x & 1)) * IP_WORDS, r);
+}
+
+// out[c] = affine(2^32 S_1 + S_0): one lane pair per combine
+__global__ void __launch_bounds__(64) k_interp_join(int ncomb, const int32_t* __restrict__ part,
+                                                    uint32_t* __restrict__ out) {
+  const int c = (int)((blockIdx.x * 64u + threadIdx.x) >> 1);
+  if (c >= ncomb) return;
+  const int h = threadIdx.x & 1;
+  const uint32_t* p = (const uint32_t*)part;
+  HJac r = hj_add(lds_get(p + ((size_t)(c * IP_NCHUNK + 1) * 2 + h) * IP_WORDS),
+                  lds_get(p + ((size_t)(c * IP_NCHUNK) * 2 + h) * IP_WORDS));
   uint32_t* o = out + (size_t)c * 48 + (lp_even() ? 0 : 12);
   if (hj_is_zero(r)) {
 #pragma unroll
@@ -191,11 +205,16 @@ namespace hbl {
 
 bool interp_g2_pair_fits(int m) { return m >= 1 && m <= 512; }
 
-hipError_t interp_g2_pair(hipStream_t s, int ncomb, int m, const uint64_t* digits, const void* pts, void* out) {
+size_t interp_g2_pair_part_bytes(int ncomb) { return (size_t)ncomb * hbs::IP_NCHUNK * 2 * hbs::IP_WORDS * 4; }
+
+hipError_t interp_g2_pair(hipStream_t s, int ncomb, int m, const uint64_t* digits, const void* pts, void* part,
+                          void* out) {
   if (ncomb <= 0) return hipSuccess;
   const size_t lds = (size_t)hbs::IP_THREADS * hbs::IP_WORDS * 4;
-  hipLaunchKernelGGL(hbs::k_interp_pair, dim3((unsigned)ncomb), dim3(hbs::IP_THREADS), lds, s, ncomb, m, digits,
-                     (const uint32_t*)pts, (uint32_t*)out);
+  hipLaunchKernelGGL(hbs::k_interp_pair, dim3((unsigned)ncomb * hbs::IP_NCHUNK), dim3(hbs::IP_THREADS), lds, s, ncomb, m,
+                     digits, (const uint32_t*)pts, (int32_t*)part);
+  hipLaunchKernelGGL(hbs::k_interp_join, dim3((unsigned)((2 * ncomb + 63) / 64)), dim3(64), 0, s, ncomb,
+                     (const int32_t*)part, (uint32_t*)out);
   return hipGetLastError();
 }
 

@@ -87,7 +87,12 @@ HP_D Fp operand(const uint32_t* sm, int h, int a, int b, int scode, int negb, in
   return x;
 }
 
-// own component of sum_t x_t * y_t (Fp2, lane-pair split of pfp.hpp h_mul_l), one reduction
+// own component of sum_t x_t * y_t (Fp2, lane-pair split of pfp.hpp h_mul_l), one reduction.
+// One wave per SIMD runs this kernel, so nothing hides a MAD's latency but the wave's own ILP: each
+// column is summed in WV_NACC independent int64 chains, joined before the Montgomery digit.
+#ifndef WV_NACC
+#define WV_NACC 4
+#endif
 template <int K>
 HP_D Fp wv_mul(const Fp (&x)[K], const Fp (&y)[K]) {
   const int32_t sm = lp_even() ? -1 : 0;
@@ -101,38 +106,40 @@ HP_D Fp wv_mul(const Fp (&x)[K], const Fp (&y)[K]) {
       Z[t][i] = (dpp<DPP_SWAP>(x[t].l[i]) ^ sm) - sm;
     }
   int32_t m[NL];
-  int64_t acc = 0;
+  int64_t carry = 0;
   Fp r;
 #pragma unroll
-  for (int k = 0; k < NL; k++) {
+  for (int k = 0; k < 2 * NL - 1; k++) {
+    int64_t acc[WV_NACC];
+#pragma unroll
+    for (int c = 0; c < WV_NACC; c++) acc[c] = 0;
+    int q = 0;
+    const int lo = k < NL ? 0 : k - NL + 1, hi = k < NL ? k : NL - 1;
 #pragma unroll
     for (int t = 0; t < K; t++)
 #pragma unroll
-      for (int i = 0; i <= k; i++) {
-        acc += (int64_t)x[t].l[i] * Y[t][k - i];
-        acc += (int64_t)Z[t][i] * W[t][k - i];
+      for (int i = lo; i <= hi; i++) {
+        acc[q++ % WV_NACC] += (int64_t)x[t].l[i] * Y[t][k - i];
+        acc[q++ % WV_NACC] += (int64_t)Z[t][i] * W[t][k - i];
       }
 #pragma unroll
-    for (int i = 0; i < k; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-    m[k] = (int32_t)(((uint32_t)acc * NP0) & (uint32_t)MASK28);
-    acc += (int64_t)m[k] * (int32_t)P_L[0];
-    acc >>= 28;
+    for (int i = lo; i <= hi; i++)
+      if (i < k) acc[q++ % WV_NACC] += (int64_t)m[i] * (int32_t)P_L[k - i];
+    int64_t col = carry;
+#pragma unroll
+    for (int c = 0; c < WV_NACC; c++) {
+      if (WV_NACC > 1) asm("" : "+v"(acc[c]));  // keep the chains apart (no reassociation into one)
+      col += acc[c];
+    }
+    if (k < NL) {
+      m[k] = (int32_t)(((uint32_t)col * NP0) & (uint32_t)MASK28);
+      col += (int64_t)m[k] * (int32_t)P_L[0];
+    } else {
+      r.l[k - NL] = (int32_t)col & MASK28;
+    }
+    carry = col >> 28;
   }
-#pragma unroll
-  for (int k = NL; k < 2 * NL - 1; k++) {
-#pragma unroll
-    for (int t = 0; t < K; t++)
-#pragma unroll
-      for (int i = k - NL + 1; i < NL; i++) {
-        acc += (int64_t)x[t].l[i] * Y[t][k - i];
-        acc += (int64_t)Z[t][i] * W[t][k - i];
-      }
-#pragma unroll
-    for (int i = k - NL + 1; i < NL; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-    r.l[k - NL] = (int32_t)acc & MASK28;
-    acc >>= 28;
-  }
-  r.l[NL - 1] = (int32_t)acc;
+  r.l[NL - 1] = (int32_t)carry;
   return r;
 }
 
@@ -164,7 +171,7 @@ HP_D Fp product_sq(const uint32_t* sm, int h, uint64_t w, uint32_t fl) {
 HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, bool act1) {
   const uint16_t ws[8] = {(uint16_t)dw.x, (uint16_t)(dw.x >> 16), (uint16_t)dw.y, (uint16_t)(dw.y >> 16),
                           (uint16_t)dw.z, (uint16_t)(dw.z >> 16), (uint16_t)dw.w, (uint16_t)(dw.w >> 16)};
-  int32_t ap[NL], at[NL];
+  int64_t ap[NL], at[NL];  // c * v fused into one v_mad_i64_i32 per limb; the sums fit int32
 #pragma unroll
   for (int i = 0; i < NL; i++) {
     ap[i] = 0;
@@ -180,21 +187,21 @@ HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, boo
       const Fp v = ld_own(sm, tm & 0xFF, h);
       if (t < j1) {
 #pragma unroll
-        for (int i = 0; i < NL; i++) ap[i] += c * v.l[i];
+        for (int i = 0; i < NL; i++) ap[i] += (int64_t)c * v.l[i];
       } else {
 #pragma unroll
-        for (int i = 0; i < NL; i++) at[i] += c * v.l[i];
+        for (int i = 0; i < NL; i++) at[i] += (int64_t)c * v.l[i];
       }
     }
   }
+  // plain terms: |limb| < 6 x 2^28 when twisted terms follow (tools/gen_wave_prog.py check_bounds)
   Fp r;
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.l[i] = ap[i];
+  for (int i = 0; i < NL; i++) r.l[i] = (int32_t)ap[i];
   if (j2) {
     Fp t;
 #pragma unroll
-    for (int i = 0; i < NL; i++) t.l[i] = at[i];
-    fp_norm(r);
+    for (int i = 0; i < NL; i++) t.l[i] = (int32_t)at[i];
     fp_norm(t);
     const Fp pt = dpp_fp<DPP_SWAP>(t);
     // xi (t0 + t1 u) = (t0 - t1) + (t0 + t1) u
@@ -208,12 +215,40 @@ HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, boo
   st_own(sm, ws[0] & 0xFF, h, r);
 }
 
+// this lane's descriptors of one stage (product: K u64 of its pair; assembly: 8 u16 of its output)
+struct StageDesc {
+  uint4 hd;
+  uint64_t p0, p1;
+  uint4 ad;
+};
+HP_D StageDesc load_stage(const uint4* hdr, int st, int pair) {
+  StageDesc d;
+  d.hd = hdr[st];
+  const uint32_t fl = d.hd.x;
+  const int kind = fl & 3, npairs = (fl >> 16) & 63, nouts = (fl >> 22) & 63;
+  d.p0 = d.p1 = 0;
+  d.ad = make_uint4(0, 0, 0, 0);
+  if (kind != 3 && pair < npairs) {
+    if (kind == 1) {
+      d.p0 = hbw::WP_PDESC[d.hd.y + 2 * pair];
+      d.p1 = hbw::WP_PDESC[d.hd.y + 2 * pair + 1];
+    } else {
+      d.p0 = hbw::WP_PDESC[d.hd.y + pair];
+    }
+  }
+  if (pair < nouts) d.ad = ((const uint4*)hbw::WP_ADESC)[d.hd.z + pair];
+  return d;
+}
+
 HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0, bool act1, const int4* tl0,
                      const int4* tl1) {
   const uint4* hdr = (const uint4*)hbw::WP_HDR;
+  // descriptors are fetched one stage ahead: their L2 latency hides behind the current stage
+  StageDesc cur = load_stage(hdr, off, pair);
 #pragma unroll 1
   for (int st = off; st < off + nst; st++) {
-    const uint4 hd = hdr[st];
+    const StageDesc nxt = load_stage(hdr, st + 1 < off + nst ? st + 1 : st, pair);
+    const uint4 hd = cur.hd;
     const uint32_t fl = hd.x;
     const int kind = fl & 3, j1 = (fl >> 2) & 7, j2 = (fl >> 5) & 7, special = (fl >> 12) & 0xF;
     const int npairs = (fl >> 16) & 63, nouts = (fl >> 22) & 63;
@@ -238,22 +273,18 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
     } else if (kind != 3 && pair < npairs) {
       Fp r;
       if (kind == 1) {
-        const uint64_t* d = hbw::WP_PDESC + hd.y + 2 * pair;
-        const uint64_t dd[2] = {d[0], d[1]};
+        const uint64_t dd[2] = {cur.p0, cur.p1};
         r = product<2>(sm, h, dd, fl);
       } else if (kind == 2) {
-        r = product_sq(sm, h, hbw::WP_PDESC[hd.y + pair], fl);
+        r = product_sq(sm, h, cur.p0, fl);
       } else {
-        const uint64_t dd[1] = {hbw::WP_PDESC[hd.y + pair]};
+        const uint64_t dd[1] = {cur.p0};
         r = product<1>(sm, h, dd, fl);
       }
       st_own(sm, hbw::WP_PROD + pair, h, r);
     }
     __syncthreads();
-    if (pair < nouts) {
-      const uint4 dw = ((const uint4*)hbw::WP_ADESC)[hd.z + pair];
-      assemble(sm, h, dw, j1, j2, act0, act1);
-    }
+    if (pair < nouts) assemble(sm, h, cur.ad, j1, j2, act0, act1);
     if (tslot >= 0) {
       int32_t w[4 * WV_LINE_Q4];
 #pragma unroll
@@ -272,6 +303,7 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
       }
     }
     __syncthreads();
+    cur = nxt;
   }
 }
 

@@ -285,7 +285,7 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_AUTO 3
 #define HBH_IMPL_PAIR 4
 #define HBH_IMPL_WAVE 5
-#define HBH_AUTO_WAVE_MAX 2048
+#define HBH_AUTO_WAVE_MAX 5120
 #define HBH_AUTO_LANE_COOP_MAX 16384
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 

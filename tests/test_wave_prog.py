@@ -54,7 +54,7 @@ def test_committed_include_is_current(progs, tmp_path):
 def test_program_shape(progs):
     for m, v in progs["variants"].items():
         assert v["nstages_miller"] <= 215 and v["nstages_fe"] <= 360, m
-        assert len(progs["slots"]) <= 256
+        assert progs["nslots"] <= 136
 
 
 @pytest.mark.parametrize("mode", W.MODES)

@@ -467,9 +467,12 @@ def schedule(ops):
 
 
 def check_bounds(op):
-    """int32 limb accumulators: per lane component, positive and negative coefficient sums <= 8."""
+    """int32 limb accumulators: per lane component, positive and negative coefficient sums <= 8, and
+    <= 6 for the plain terms of an output with twisted terms (the kernel adds the normalised twisted
+    sum and its partner component, up to 2 x 2^28 per limb, before the final carry pass)."""
     for o in op.outs:
         for terms in (o.plain, o.tw):
+            limit = COEF_LIMIT - 2 if (terms is o.plain and o.tw) else COEF_LIMIT
             for h in (0, 1):
                 pos = neg = 0
                 for (_, c, cj) in terms:
@@ -478,7 +481,7 @@ def check_bounds(op):
                         pos += ce
                     else:
                         neg -= ce
-                assert pos <= COEF_LIMIT and neg <= COEF_LIMIT, (op.name, o.dst, terms)
+                assert pos <= limit and neg <= limit, (op.name, o.dst, terms)
                 for (_, c, _) in terms:
                     assert -8 <= c <= 7, (op.name, c)
 
@@ -748,7 +751,7 @@ def emulate(prog, sides, conj=False):
 
     run(*prog["miller"])
     run(*prog["fe"])
-    f = [mem[S["E%d" % k]] for k in range(6)]
+    f = [mem[prog["slots_fe"]["E%d" % k]] for k in range(6)]
     if conj:
         f = [f[k] if k % 2 == 0 else f2scale(f[k], -1) for k in range(6)]
     return f
@@ -758,33 +761,70 @@ def emulate(prog, sides, conj=False):
 MODES = ["WW", "WT", "TW", "TT"]
 
 
+def allocate(b, stages):
+    """Physical LDS slots by live range: the fixed slots (constants, F, the two sides, PROD) keep
+    their indices; every other name (a TLOAD triple as one block of 3) gets the lowest free index
+    whose previous occupant was last read in an earlier stage than this name's first write."""
+    fixed = Builder("fixed").slots
+    first, last = {}, {}
+    for t, st in enumerate(stages):
+        for op in st.ops:
+            for n in op.reads_prod() | op.reads_asm():
+                last[n] = max(last.get(n, -1), t)
+            for n in op.writes():
+                first[n] = min(first.get(n, 1 << 30), t)
+                last[n] = max(last.get(n, -1), t)
+    units, seen = [], set(fixed)
+    for st in stages:
+        for op in st.ops:
+            if op.tload and op.tload[3][0] not in seen:
+                units.append(list(op.tload[3]))
+                seen |= set(op.tload[3])
+    for n in b.slots:
+        if n not in seen:
+            units.append([n])
+            seen.add(n)
+    span = []
+    for u in units:
+        s0 = min(first.get(n, last.get(n, 0)) for n in u)
+        e0 = max(last.get(n, s0) for n in u)
+        span.append((s0, e0, u))
+    span.sort(key=lambda x: (x[0], x[2][0]))
+    busy = {}
+    mapping = dict(fixed)
+    base0 = len(fixed)
+    for (s0, e0, u) in span:
+        k = base0
+        while any(busy.get(k + j, -1) >= s0 for j in range(len(u))):
+            k += 1
+        for j, n in enumerate(u):
+            mapping[n] = k + j
+            busy[k + j] = e0
+    assert max(mapping.values()) < 256
+    return mapping
+
+
 def build():
-    """One Builder per WALK/TABLE combination for the Miller part; the final exponentiation is
-    built once (same slot map: its slots are appended after the largest Miller map)."""
-    progs = {}
-    fe_b = None
+    """One program per WALK/TABLE combination for the Miller part and one final exponentiation,
+    each scheduled into stages and then given physical LDS slots by live range (allocate)."""
+    out = {"variants": {}}
+    fe = Builder("fe")
+    fe.final_exp()
+    fe_stages = schedule(fe.ops)
+    fe.slots = allocate(fe, fe_stages)
+    fe_enc = encode(fe, fe_stages)
+    nslots = max(fe.slots.values()) + 1
     for m in MODES:
         b = Builder(m)
         b.miller((m[0], m[1]))
-        progs[m] = b
-    # common slot map: union in a fixed order (Miller maps first, then the final exponentiation)
-    common = Builder("common")
-    for m in MODES:
-        for name in progs[m].slots:
-            common.slot(name)
-    fe_ops_builder = Builder("fe")
-    fe_ops_builder.slots = common.slots
-    fe_ops_builder.final_exp()
-    slots = fe_ops_builder.slots
-    out = {"slots": slots, "variants": {}}
-    fe_stages = schedule(fe_ops_builder.ops)
-    fe_enc = encode(fe_ops_builder, fe_stages)
-    for m in MODES:
-        progs[m].slots = slots
-        st = schedule(progs[m].ops)
-        out["variants"][m] = {"miller": encode(progs[m], st), "fe": fe_enc, "slots": slots,
+        st = schedule(b.ops)
+        b.slots = allocate(b, st)
+        nslots = max(nslots, max(b.slots.values()) + 1)
+        out["variants"][m] = {"miller": encode(b, st), "fe": fe_enc, "slots": b.slots, "slots_fe": fe.slots,
                               "nstages_miller": len(st), "nstages_fe": len(fe_stages),
                               "stages_miller": st, "stages_fe": fe_stages}
+    out["nslots"] = nslots
+    out["slots"] = fe.slots
     return out
 
 
@@ -794,7 +834,7 @@ def emit(out, path):
              "// pairing kernel (k_wave.hip): 4 u32 header per stage, u64 product descriptors, 8 x u16",
              "// assembly descriptors (formats in tools/gen_wave_prog.py).",
              "#pragma once", "#include <stdint.h>", "namespace hbw {",
-             "constexpr int WP_NSLOTS = %d;" % len(slots),
+             "constexpr int WP_NSLOTS = %d;" % out["nslots"],
              "constexpr int WP_F = %d;" % slots["F0"],
              "constexpr int WP_E = %d;" % slots["E0"],
              "constexpr int WP_PROD = %d;" % slots["PROD0"],
@@ -845,7 +885,7 @@ def stats(out):
         v = out["variants"][m]
         c = sum(cost[s.kind] for s in v["stages_miller"]) + sum(cost[s.kind] for s in v["stages_fe"])
         print("%s: %d Miller stages + %d final-exp stages, %.0f M1-equivalents, %d slots" % (
-            m, v["nstages_miller"], v["nstages_fe"], c, len(out["slots"])))
+            m, v["nstages_miller"], v["nstages_fe"], c, out["nslots"]))
 
 
 if __name__ == "__main__":
