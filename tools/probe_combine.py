@@ -35,7 +35,7 @@ h = eng.g2_mul([G2], [rng.randrange(1, R)])[0]
 idx = list(range(3, 3 + t + 1))
 sig = eng.g2_mul([h] * (t + 1), [sks[i] for i in idx])
 out = {}
-for name, impl in (("auto", IMPL_AUTO), ("lane_coop", IMPL_LANE_COOP), ("pair", IMPL_PAIR)):
+for name, impl in (("auto", IMPL_AUTO), ("lane_coop", IMPL_LANE_COOP)):
     eng.set_pairing_impl(impl)
     for _ in range(2):
         eng.combine_verify_g2(t, [idx], [sig], mpk, [h])
