@@ -266,7 +266,11 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
       }
     }
     if (special == 1) {
+#ifdef WV_SKIP_INV  // timing experiment only: wrong verdicts
+      if (false) {
+#else
       if (pair == 0) {
+#endif
         const Fp v = ld_own(sm, hd.w & 0xFF, h);
         st_own(sm, (hd.w >> 8) & 0xFF, h, fp_reduce(h_inv_vartime(v)));
       }

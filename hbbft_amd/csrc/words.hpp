@@ -12,10 +12,10 @@
 
 namespace hb {
 
-// Variable-time inverse for public values (HB_FP_LATENCY kernels: the single-thread affine output of
-// combines and scalar multiples, whose inputs and results are public): binary extended Euclid over
-// canonical 32-bit words, ~2 x 381 shift/subtract steps instead of 381 squarings + 190 products.
-// Divergent across lanes, so kernels where every lane inverts keep the uniform Fermat form.
+// Variable-time inverse for public values (the affine outputs of combines and scalar multiples,
+// the final exponentiation's one inversion in the wave kernel): a batched binary GCD over canonical
+// 32-bit words.  Divergent across lanes, so kernels where every lane inverts keep the uniform
+// Fermat form.
 template <int N>
 HW_HD bool words_is_one(const uint32_t* x) {
   uint32_t o = x[0] ^ 1u;
@@ -53,38 +53,192 @@ HW_HD bool words_geq(const uint32_t* x, const uint32_t* y) {
     if (x[i] != y[i]) return x[i] > y[i];
   return true;
 }
-// out = a^-1 mod `mod` (odd), a canonical and nonzero
+// Bit length of an N-word value (0 for zero); branch-free over the words so that x stays in VGPRs.
 template <int N>
-HW_HD void words_inv_vartime(const uint32_t* a, const uint32_t* mod, uint32_t* out) {
-  uint32_t u[N], v[N], x1[N], x2[N];
+HW_HD int words_bitlen(const uint32_t* x) {
+  int len = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    if (x[i]) len = 32 * i + 32 - __builtin_clz(x[i]);
+  return len;
+}
+// 64 bits of x starting at bit s (bits beyond the top read as zero), selected without dynamic
+// register indexing
+template <int N>
+HW_HD uint64_t words_bits64(const uint32_t* x, int s) {
+  const int w = s >> 5, sh = s & 31;
+  uint32_t lo = 0, mid = 0, hi = 0;
+#pragma unroll
   for (int i = 0; i < N; i++) {
-    u[i] = a[i];
-    v[i] = mod[i];
-    x1[i] = 0;
-    x2[i] = 0;
+    lo = (i == w) ? x[i] : lo;
+    mid = (i == w + 1) ? x[i] : mid;
+    hi = (i == w + 2) ? x[i] : hi;
   }
-  x1[0] = 1;
-  while (!words_is_one<N>(u) && !words_is_one<N>(v)) {
-    while ((u[0] & 1) == 0) {
-      words_shr1<N>(u, 0);
-      const uint32_t c = (x1[0] & 1) ? words_add<N>(x1, mod) : 0;
-      words_shr1<N>(x1, c);
+  const uint64_t v = (uint64_t)lo | ((uint64_t)mid << 32);
+  return sh ? (v >> sh) | ((uint64_t)hi << (64 - sh)) : v;
+}
+// t = x * fx + y * fy (x, y < 2^(32N) unsigned; |fx|, |fy| <= 2^31) as an (N+2)-word two's-complement
+// value, shifted right (arithmetically) by 31 bits into N+1 words
+template <int N>
+HW_HD void words_lincomb_shr31(const uint32_t* x, int64_t fx, const uint32_t* y, int64_t fy, uint32_t* out) {
+  uint32_t t[N + 2];
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const int64_t p1 = (int64_t)x[i] * fx, p2 = (int64_t)y[i] * fy;
+    const int64_t sw = (int64_t)(uint32_t)p1 + (int64_t)(uint32_t)p2 + c;
+    t[i] = (uint32_t)sw;
+    c = (sw >> 32) + (p1 >> 32) + (p2 >> 32);
+  }
+  t[N] = (uint32_t)c;
+  t[N + 1] = (uint32_t)(c >> 32);
+#pragma unroll
+  for (int i = 0; i <= N; i++) out[i] = (t[i] >> 31) | (t[i + 1] << 1);
+}
+template <int N>
+HW_HD bool words_neg_if(uint32_t* x, bool neg) {  // two's-complement negation of N words when neg
+  if (!neg) return false;
+  uint64_t c = 1;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    c += (uint64_t)(uint32_t)~x[i];
+    x[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return true;
+}
+
+// out = a^-1 mod `mod` (odd modulus of at most 32N - 2 bits, a canonical); 0 when a is 0 or not
+// invertible.  Variable time, for public values only.  T. Pornin's optimized binary GCD
+// (eprint 2020/972, Algorithm 2): the binary GCD's 2 len(m) - 1 divsteps in rounds of 31, each round
+// deciding on 64-bit approximations of (a, b) -- the low 31 bits and the top 33 bits -- and then
+// applying the round's 2x2 update matrix to the full a, b and to the coefficients u, v (divided
+// by 2^31 mod m, Montgomery style).  ~25 rounds for a 381-bit modulus instead of ~760 multiword
+// shift / subtract steps.  Fixed round count: no data-dependent termination.
+template <int N>
+HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* out) {
+  uint32_t a[N + 1], b[N + 1], u[N + 1], v[N + 1];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    a[i] = y[i];
+    b[i] = mod[i];
+    u[i] = 0;
+    v[i] = 0;
+  }
+  a[N] = b[N] = u[N] = v[N] = 0;
+  u[0] = 1;
+  // -mod^-1 mod 2^32 (Newton)
+  uint32_t inv = mod[0];
+  for (int k = 0; k < 5; k++) inv *= 2u - mod[0] * inv;
+  const uint32_t minv = 0u - inv;
+  const int rounds = (2 * words_bitlen<N>(mod) - 1 + 30) / 31;
+  for (int r = 0; r < rounds; r++) {
+    int n = words_bitlen<N>(a);
+    const int nb = words_bitlen<N>(b);
+    if (nb > n) n = nb;
+    if (n < 64) n = 64;
+    uint64_t ab = ((uint64_t)a[0] & 0x7fffffffu) | (words_bits64<N>(a, n - 33) << 31);
+    uint64_t bb = ((uint64_t)b[0] & 0x7fffffffu) | (words_bits64<N>(b, n - 33) << 31);
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    for (int j = 0; j < 31; j++) {
+      if (ab & 1) {
+        if (ab < bb) {
+          const uint64_t t = ab;
+          ab = bb;
+          bb = t;
+          int64_t q = f0;
+          f0 = f1;
+          f1 = q;
+          q = g0;
+          g0 = g1;
+          g1 = q;
+        }
+        ab = (ab - bb) >> 1;
+        f0 -= f1;
+        g0 -= g1;
+      } else {
+        ab >>= 1;
+      }
+      f1 *= 2;
+      g1 *= 2;
     }
-    while ((v[0] & 1) == 0) {
-      words_shr1<N>(v, 0);
-      const uint32_t c = (x2[0] & 1) ? words_add<N>(x2, mod) : 0;
-      words_shr1<N>(x2, c);
+    uint32_t na[N + 1], nbw[N + 1];
+    words_lincomb_shr31<N>(a, f0, b, g0, na);
+    words_lincomb_shr31<N>(a, f1, b, g1, nbw);
+    if (words_neg_if<N + 1>(na, (int32_t)na[N] < 0)) {
+      f0 = -f0;
+      g0 = -g0;
     }
-    if (words_geq<N>(u, v)) {
-      words_sub<N>(u, v);
-      if (words_sub<N>(x1, x2)) words_add<N>(x1, mod);
-    } else {
-      words_sub<N>(v, u);
-      if (words_sub<N>(x2, x1)) words_add<N>(x2, mod);
+    if (words_neg_if<N + 1>(nbw, (int32_t)nbw[N] < 0)) {
+      f1 = -f1;
+      g1 = -g1;
+    }
+#pragma unroll
+    for (int i = 0; i <= N; i++) {
+      a[i] = na[i];
+      b[i] = nbw[i];
+    }
+    // (u, v) <- ((u f0 + v g0) / 2^31, (u f1 + v g1) / 2^31) mod m
+    uint32_t nu[2][N + 1];
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+      const int64_t fu = side ? f1 : f0, fv = side ? g1 : g0;
+      uint32_t t[N + 2];
+      int64_t c = 0;
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        const int64_t p1 = (int64_t)u[i] * fu, p2 = (int64_t)v[i] * fv;
+        const int64_t sw = (int64_t)(uint32_t)p1 + (int64_t)(uint32_t)p2 + c;
+        t[i] = (uint32_t)sw;
+        c = (sw >> 32) + (p1 >> 32) + (p2 >> 32);
+      }
+      t[N] = (uint32_t)c;
+      t[N + 1] = (uint32_t)(c >> 32);
+      // + q m with q = -t mod^-1 mod 2^31: the sum is divisible by 2^31
+      const uint64_t q = (uint64_t)((t[0] * minv) & 0x7fffffffu);
+      uint64_t cc = 0;
+#pragma unroll
+      for (int i = 0; i < N; i++) {
+        cc += (uint64_t)t[i] + q * mod[i];
+        t[i] = (uint32_t)cc;
+        cc >>= 32;
+      }
+#pragma unroll
+      for (int i = N; i < N + 2; i++) {
+        cc += (uint64_t)t[i];
+        t[i] = (uint32_t)cc;
+        cc >>= 32;
+      }
+      uint32_t w[N + 1];
+#pragma unroll
+      for (int i = 0; i <= N; i++) w[i] = (t[i] >> 31) | (t[i + 1] << 1);
+      // |w| < 3m: bring into [0, m)
+      for (int k = 0; k < 3 && (int32_t)w[N] < 0; k++) {
+        uint64_t ac = 0;
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+          ac += (uint64_t)w[i] + mod[i];
+          w[i] = (uint32_t)ac;
+          ac >>= 32;
+        }
+        w[N] += (uint32_t)ac;
+      }
+      for (int k = 0; k < 3 && (w[N] != 0 || words_geq<N>(w, mod)); k++) {
+        const uint32_t br = words_sub<N>(w, mod);
+        w[N] -= br;
+      }
+#pragma unroll
+      for (int i = 0; i <= N; i++) nu[side][i] = w[i];
+    }
+#pragma unroll
+    for (int i = 0; i <= N; i++) {
+      u[i] = nu[0][i];
+      v[i] = nu[1][i];
     }
   }
-  const bool one_u = words_is_one<N>(u);
-  for (int i = 0; i < N; i++) out[i] = one_u ? x1[i] : x2[i];
+  bool one = b[N] == 0 && words_is_one<N>(b);
+#pragma unroll
+  for (int i = 0; i < N; i++) out[i] = one ? v[i] : 0u;
 }
 
 }  // namespace hb
