@@ -684,7 +684,10 @@ void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* di
 // lane-pair form (digits + k_interp_pair); many take k_interp_endo (throughput form).  With the x
 // values on the host and at most HOST_DIGITS_MAX combines, the digits are computed on the host and
 // uploaded (status too) instead of running k_interp_digits.
-constexpr size_t INTERP_PAIR_MAX = 64;
+#ifndef HBH_INTERP_PAIR_MAX
+#define HBH_INTERP_PAIR_MAX 384  // measured crossover with k_interp_endo<Fp2>: 100 combines 5.25 -> 2.46 ms, 1,024: 11.9 vs 15.8 ms
+#endif
+constexpr size_t INTERP_PAIR_MAX = HBH_INTERP_PAIR_MAX;
 constexpr size_t HOST_DIGITS_MAX = 2;
 int launch_combine_g2(hbh_engine* e, hipStream_t s, size_t ncomb, size_t m, const uint32_t* d_xs, const void* d_pts,
                       void* d_out, int* d_status, const uint32_t* h_xs = nullptr) {
