@@ -141,14 +141,15 @@ def _sign_batch(engine, rng, ndocs, per_doc):
     return ([pks[i % per_doc] for i in range(n)], sigs, hs, [i // per_doc for i in range(n)], want)
 
 
-def test_dev_calls_on_two_streams(engine):
+@pytest.mark.parametrize("impl", [4, 5], ids=["pair", "wave"])
+def test_dev_calls_on_two_streams(engine, impl):
     """Two hbh_verify_pairing_eq_dev calls queued back-to-back on two different streams:
     the second call's line tables must not overwrite the first call's while its kernels still read
     them -- the engine orders calls with its completion event.  Both verdict arrays are exact."""
-    from hbbft_amd._lib import IMPL_AUTO, IMPL_PAIR
+    from hbbft_amd._lib import IMPL_AUTO
     rng = random.Random(2024)
     batches = [_sign_batch(engine, rng, 64, 32), _sign_batch(engine, rng, 48, 32)]
-    engine.set_pairing_impl(IMPL_PAIR)
+    engine.set_pairing_impl(impl)
     try:
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
         keep, outs = [], []
@@ -168,16 +169,17 @@ def test_dev_calls_on_two_streams(engine):
         engine.set_pairing_impl(IMPL_AUTO)
 
 
-def test_dev_index_out_of_range_rejects(engine):
-    """HBH_IMPL_PAIR validates device index arrays in-kernel: an index >= its table size gives
-    verdict 0 for that item only (never a read past the table)."""
-    from hbbft_amd._lib import IMPL_AUTO, IMPL_PAIR
+@pytest.mark.parametrize("impl", [4, 5], ids=["pair", "wave"])
+def test_dev_index_out_of_range_rejects(engine, impl):
+    """HBH_IMPL_PAIR and HBH_IMPL_WAVE validate device index arrays in-kernel: an index >= its table
+    size gives verdict 0 for that item only (never a read past the table)."""
+    from hbbft_amd._lib import IMPL_AUTO
     rng = random.Random(9)
     pks, sigs, hs, di, want = _sign_batch(engine, rng, 8, 16)
     di = list(di)
     di[5] = 8          # == table size
     di[77] = 1 << 30   # far out of range
-    engine.set_pairing_impl(IMPL_PAIR)
+    engine.set_pairing_impl(impl)
     try:
         d_pk, d_sg, d_h = dev(b"".join(pks)), dev(b"".join(sigs)), dev(b"".join(hs))
         d_di = dev(np.array(di, dtype=np.uint32).tobytes(), torch.int32)

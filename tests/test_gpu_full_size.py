@@ -70,6 +70,21 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
         assert cbls.verify_g2(b["pks"][i % N], b["sigs"][i], b["hashes"][i // N]) == bool(v[i]), i
 
 
+def test_config1_wave_at_auto_threshold(engine, sign_batch):
+    """The wave-per-check kernel on the largest batch AUTO gives it (HBH_AUTO_WAVE_MAX = 5,120
+    checks: 80 documents of configs[1]), walking both G2 sides: verdicts equal the construction."""
+    from hbbft_amd._lib import IMPL_WAVE
+    b = sign_batch
+    n = 5120
+    engine.set_pairing_impl(IMPL_WAVE)
+    try:
+        v = engine.verify_sig_shares([b["pks"][i % N] for i in range(n)], b["sigs"][:n], b["hashes"][:n // N],
+                                     [i // N for i in range(n)])
+    finally:
+        engine.set_pairing_impl(IMPL_AUTO)
+    assert v == b["expected"][:n]
+
+
 def test_config1_combines(engine, sign_batch):
     """combine_and_verify_sig for all 1,024 documents (first 22 valid shares) in one call."""
     b = sign_batch
