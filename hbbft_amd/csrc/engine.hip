@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -1021,6 +1022,10 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
     }
   }
   const size_t nrow = row_part.size();
+  // acks in order of y: the lanes of a wave then run the same small-scalar double-and-add
+  std::vector<uint32_t> order(nack);
+  for (size_t a = 0; a < nack; a++) order[a] = (uint32_t)a;
+  std::stable_sort(order.begin(), order.end(), [ys](uint32_t i, uint32_t j) { return ys[i] < ys[j]; });
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = e->stream;
@@ -1029,7 +1034,7 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
     if (rc_) return rc_;
   }
   HBH_CHECK(e->in_a.ensure(nparts * ncoef * HBH_G1_BYTES));
-  HBH_CHECK(e->in_b.ensure(nrow * 8 + nack * 8));
+  HBH_CHECK(e->in_b.ensure(nrow * 8 + nack * 12));
   HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
   HBH_CHECK(e->work.ensure(nrow * (t + 1) * HBH_G1_BYTES));
   HBH_CHECK(e->out_v.ensure(nack));
@@ -1037,18 +1042,20 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   uint32_t* d_rx = d_rp + nrow;
   uint32_t* d_ro = d_rx + nrow;
   uint32_t* d_y = d_ro + nack;
+  uint32_t* d_ord = d_y + nack;
   HBH_CHECK(hipMemcpyAsync(e->in_a.p, commits, nparts * ncoef * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(d_rp, row_part.data(), nrow * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(d_rx, row_x.data(), nrow * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(d_ro, row_of.data(), nack * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(d_y, ys, nack * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_ord, order.data(), nack * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
   HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, e->in_a.p, d_rp, d_rx, e->work.p));
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
-  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
-                             (uint8_t*)e->out_v.p));
+  HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
+                                  (uint8_t*)e->out_v.p, d_ord));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, nack, hipMemcpyDeviceToHost, s));
   {
@@ -1155,8 +1162,8 @@ int hbh_bivar_ack_check_dev(hbh_engine* e, void* stream, size_t nack, int t, con
   HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, d_commits, d_row_part, d_row_x, e->work.p));
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
-  HBH_CHECK(hbl::bivar_check(s, (int)nack, t, e->work.p, d_row_of, d_ys, (const uint32_t*)d_vals, e->fbtab.p,
-                             d_verdicts));
+  HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, e->work.p, d_row_of, d_ys, (const uint32_t*)d_vals, e->fbtab.p,
+                                  d_verdicts, nullptr));
   e->timer.end(s, tm);
   return end_call(e, s);
 }

@@ -452,12 +452,16 @@ __global__ void __launch_bounds__(256) k_index_plus_one(int n, int m, const uint
 
 // BivarCommitment::evaluate(x, y) == G1::one() * val  (src/sync_key_gen.rs:542), from the rows
 // R = row(x): evaluate(x, y) = sum_j R_j y^j (Horner with the small y).  One thread per ack.
+// order (optional): thread k checks ack order[k] -- the host sorts acks by y so that the lanes of a
+// wave share y and the small-scalar double-and-add of the Horner steps does not diverge.
 __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint32_t* __restrict__ rows,
                                                      const uint32_t* __restrict__ row_idx,
                                                      const uint32_t* __restrict__ ys, const uint32_t* __restrict__ vals,
-                                                     const uint32_t* __restrict__ fbtab, uint8_t* __restrict__ verdict) {
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= nack) return;
+                                                     const uint32_t* __restrict__ fbtab, const uint32_t* __restrict__ order,
+                                                     uint8_t* __restrict__ verdict) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nack) return;
+  const int a = order ? (int)order[k] : k;
   const uint32_t* R = rows + (size_t)row_idx[a] * (t + 1) * G1_WORDS;
   const uint32_t y = ys[a];
   Jac<Fp> acc = jac_zero<Fp>();
@@ -468,9 +472,9 @@ __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint
     load_g1(R + (size_t)j * G1_WORDS, rx, ry, inf);
     if (!inf) acc = jac_add_affine(acc, rx, ry);
   }
-  uint32_t k[8];
-  for (int j = 0; j < 8; j++) k[j] = vals[(size_t)a * 8 + j];
-  const Jac<Fp> w = fb_mul(fbtab, k);
+  uint32_t ks[8];
+  for (int j = 0; j < 8; j++) ks[j] = vals[(size_t)a * 8 + j];
+  const Jac<Fp> w = fb_mul(fbtab, ks);
   verdict[a] = jac_eq(acc, w) ? 1 : 0;
 }
 
@@ -550,10 +554,10 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
   return hipGetLastError();
 }
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
-                       const uint32_t* vals, const void* fbtab, uint8_t* verdict) {
+                       const uint32_t* vals, const void* fbtab, uint8_t* verdict, const uint32_t* order) {
   if (nack <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_bivar_check, grid_for(nack), dim3(256), 0, s, nack, t, (const uint32_t*)rows, row_idx, ys,
-                     vals, (const uint32_t*)fbtab, verdict);
+                     vals, (const uint32_t*)fbtab, order, verdict);
   return hipGetLastError();
 }
 

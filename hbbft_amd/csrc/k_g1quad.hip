@@ -1,0 +1,253 @@
+// BivarCommitment::evaluate(x, y) == g1 * val for SyncKeyGen Ack checks (src/sync_key_gen.rs:542)
+// on LANE QUADS (gfx950).
+//
+// One node checks ~N^2 acks at once, each a serial G1 chain: the Horner evaluation of the row
+// polynomial at the small y (t + 1 steps of a 7-bit double-and-add plus a mixed addition) and g1 *
+// val from the comb table.  10,000 acks are 0.15 waves per SIMD with one lane per ack, so the chain
+// length is the time.  Here four lanes hold the same point and split every group operation's
+// independent Fp products between them, one product per lane per round, exchanging results with DPP
+// quad broadcasts: a doubling takes 3 rounds instead of 7 serial products, a mixed or general
+// addition 5 instead of 11 / 16.  g1 * val: each lane adds its quarter of the 32 comb windows on its
+// own, then the quad joins the four partial sums.  Formulas: dbl-2009-l, madd-2007-bl, add-2007-bl
+// (the group law of curve.hpp) on the signed-limb Fp of sfp.hpp; the verdict is point equality, so
+// it is the one of k_bivar_check.
+#include "launch.hpp"
+#include "sfp.hpp"
+
+namespace hbs {
+
+constexpr int Q_FB_WINDOWS = 32, Q_FB_ROW = 256, Q_G1_WORDS = 24;
+
+struct QJ {
+  Fp x, y, z;
+};
+
+__device__ __forceinline__ int q_lane() { return threadIdx.x & 3; }
+template <int CTRL>
+__device__ __forceinline__ Fp q_dpp(const Fp& a) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = __builtin_amdgcn_mov_dpp(a.l[i], CTRL, 0xF, 0xF, true);
+  return r;
+}
+__device__ __forceinline__ Fp q_sel4(int q, const Fp& a0, const Fp& a1, const Fp& a2, const Fp& a3) {
+  return fp_sel(q == 0, a0, fp_sel(q == 1, a1, fp_sel(q == 2, a2, a3)));
+}
+// one round: lane k of the quad forms a_k * b_k; every lane gets all four products
+__device__ __forceinline__ void q4(const Fp& a0, const Fp& b0, const Fp& a1, const Fp& b1, const Fp& a2, const Fp& b2,
+                                   const Fp& a3, const Fp& b3, Fp& r0, Fp& r1, Fp& r2, Fp& r3) {
+  const int q = q_lane();
+  const Fp r = fp_mul(q_sel4(q, a0, a1, a2, a3), q_sel4(q, b0, b1, b2, b3));
+  r0 = q_dpp<0x00>(r);
+  r1 = q_dpp<0x55>(r);
+  r2 = q_dpp<0xAA>(r);
+  r3 = q_dpp<0xFF>(r);
+}
+__device__ __forceinline__ void q3(const Fp& a0, const Fp& b0, const Fp& a1, const Fp& b1, const Fp& a2, const Fp& b2,
+                                   Fp& r0, Fp& r1, Fp& r2) {
+  const int q = q_lane();
+  const Fp r = fp_mul(q_sel4(q, a0, a1, a2, a2), q_sel4(q, b0, b1, b2, b2));
+  r0 = q_dpp<0x00>(r);
+  r1 = q_dpp<0x55>(r);
+  r2 = q_dpp<0xAA>(r);
+}
+__device__ __forceinline__ void q2(const Fp& a0, const Fp& b0, const Fp& a1, const Fp& b1, Fp& r0, Fp& r1) {
+  const bool odd = (q_lane() & 1) != 0;
+  const Fp r = fp_mul(fp_sel(odd, a1, a0), fp_sel(odd, b1, b0));
+  r0 = q_dpp<0x00>(r);
+  r1 = q_dpp<0x55>(r);
+}
+
+__device__ __forceinline__ bool qj_zero(const QJ& p) { return fp_is_zero(p.z); }
+__device__ __forceinline__ QJ qj_inf() { return {fp_one(), fp_one(), fp_zero()}; }
+
+// dbl-2009-l, 3 rounds; inputs reduced, outputs reduced
+__device__ __forceinline__ QJ g1q_dbl(const QJ& p) {
+  Fp A, B, YZ, C, XB2, F, u;
+  q3(p.x, p.x, p.y, p.y, p.y, p.z, A, B, YZ);
+  const Fp E = fp_lin(3, A, 0, A);
+  const Fp XB = fp_add(p.x, B);
+  q3(B, B, XB, XB, E, E, C, XB2, F);
+  const Fp D = fp_reduce(fp_lin(2, fp_sub(fp_sub(XB2, A), C), 0, C));
+  QJ r;
+  r.x = fp_reduce(fp_sub(F, fp_add(D, D)));
+  u = fp_mul(E, fp_sub(D, r.x));
+  r.y = fp_reduce(fp_sub(u, fp_lin(8, C, 0, C)));
+  r.z = fp_reduce(fp_add(YZ, YZ));
+  return r;
+}
+
+// madd-2007-bl: p + (x2, y2) with (x2, y2) affine and not infinity, 5 rounds
+__device__ __forceinline__ QJ g1q_add_affine(const QJ& p, const Fp& x2, const Fp& y2) {
+  if (qj_zero(p)) return {x2, y2, fp_one()};
+  Fp Z1Z1, YZ, U2, S2;
+  q2(p.z, p.z, y2, p.z, Z1Z1, YZ);
+  q2(x2, Z1Z1, YZ, Z1Z1, U2, S2);
+  const Fp H = fp_reduce(fp_sub(U2, p.x));
+  const Fp rr = fp_reduce(fp_lin(2, S2, -2, p.y));
+  if (fp_is_zero(H)) {
+    if (fp_is_zero(rr)) return g1q_dbl(p);
+    return qj_inf();
+  }
+  Fp HH, RR, ZH, J, V, EV, YJ;
+  q3(H, H, rr, rr, p.z, H, HH, RR, ZH);
+  const Fp I = fp_lin(4, HH, 0, HH);
+  q2(H, I, p.x, I, J, V);
+  QJ r;
+  r.x = fp_reduce(fp_sub(fp_sub(RR, J), fp_add(V, V)));
+  q2(rr, fp_sub(V, r.x), p.y, J, EV, YJ);
+  r.y = fp_reduce(fp_sub(EV, fp_add(YJ, YJ)));
+  r.z = fp_reduce(fp_add(ZH, ZH));
+  return r;
+}
+
+// add-2007-bl (general), 5 rounds
+__device__ __forceinline__ QJ g1q_add(const QJ& p, const QJ& q) {
+  if (qj_zero(p)) return q;
+  if (qj_zero(q)) return p;
+  Fp Z1Z1, Z2Z2, Y1Z2, Y2Z1, U1, U2, S1, S2;
+  q4(p.z, p.z, q.z, q.z, p.y, q.z, q.y, p.z, Z1Z1, Z2Z2, Y1Z2, Y2Z1);
+  q4(p.x, Z2Z2, q.x, Z1Z1, Y1Z2, Z2Z2, Y2Z1, Z1Z1, U1, U2, S1, S2);
+  const Fp H = fp_reduce(fp_sub(U2, U1));
+  const Fp rr = fp_reduce(fp_lin(2, S2, -2, S1));
+  if (fp_is_zero(H)) {
+    if (fp_is_zero(rr)) return g1q_dbl(p);
+    return qj_inf();
+  }
+  Fp I, RR, Z12, J, V, Z12H, EV, SJ;
+  const Fp H2 = fp_add(H, H);
+  q3(H2, H2, rr, rr, p.z, q.z, I, RR, Z12);
+  q3(H, I, U1, I, Z12, H, J, V, Z12H);
+  QJ r;
+  r.x = fp_reduce(fp_sub(fp_sub(RR, J), fp_add(V, V)));
+  q2(rr, fp_sub(V, r.x), S1, J, EV, SJ);
+  r.y = fp_reduce(fp_sub(EV, fp_add(SJ, SJ)));
+  r.z = fp_reduce(fp_add(Z12H, Z12H));
+  return r;
+}
+
+// k * p for a small k (double-and-add from the top bit)
+__device__ __forceinline__ QJ g1q_mul_small(const QJ& p, uint32_t k) {
+  if (k == 0) return qj_inf();
+  const int top = 31 - __builtin_clz(k);
+  QJ acc = p;
+#pragma unroll 1
+  for (int i = top - 1; i >= 0; i--) {
+    acc = g1q_dbl(acc);
+    if ((k >> i) & 1) acc = g1q_add(acc, p);
+  }
+  return acc;
+}
+
+// P == Q as group elements, 2 rounds
+__device__ __forceinline__ bool g1q_eq(const QJ& p, const QJ& q) {
+  const bool pz = qj_zero(p), qz = qj_zero(q);
+  if (pz || qz) return pz && qz;
+  Fp Z1Z1, Z2Z2, Y1Z2, Y2Z1, a, b, c, d;
+  q4(p.z, p.z, q.z, q.z, p.y, q.z, q.y, p.z, Z1Z1, Z2Z2, Y1Z2, Y2Z1);
+  q4(p.x, Z2Z2, q.x, Z1Z1, Y1Z2, Z2Z2, Y2Z1, Z1Z1, a, b, c, d);
+  return fp_is_zero(fp_sub(a, b)) && fp_is_zero(fp_sub(c, d));
+}
+
+__device__ __forceinline__ bool load_aff(const uint32_t* __restrict__ w, Fp& x, Fp& y) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int k = 0; k < Q_G1_WORDS; k++) o |= w[k];
+  x = fp_from_words(w);
+  y = fp_from_words(w + 12);
+  return o == 0;
+}
+
+// single-lane mixed addition (this lane's own comb windows)
+__device__ __forceinline__ QJ g1_madd_lane(const QJ& p, const Fp& x2, const Fp& y2);
+__device__ __forceinline__ QJ g1_dbl_lane(const QJ& p) {
+  const Fp A = fp_sqr(p.x);
+  const Fp B = fp_sqr(p.y);
+  const Fp C = fp_sqr(B);
+  const Fp D = fp_reduce(fp_lin(2, fp_sub(fp_sub(fp_sqr(fp_add(p.x, B)), A), C), 0, C));
+  const Fp E = fp_lin(3, A, 0, A);
+  QJ r;
+  r.x = fp_reduce(fp_sub(fp_sqr(E), fp_add(D, D)));
+  r.y = fp_reduce(fp_sub(fp_mul(E, fp_sub(D, r.x)), fp_lin(8, C, 0, C)));
+  const Fp yz = fp_mul(p.y, p.z);
+  r.z = fp_reduce(fp_add(yz, yz));
+  return r;
+}
+__device__ __forceinline__ QJ g1_madd_lane(const QJ& p, const Fp& x2, const Fp& y2) {
+  if (qj_zero(p)) return {x2, y2, fp_one()};
+  const Fp Z1Z1 = fp_sqr(p.z);
+  const Fp U2 = fp_mul(x2, Z1Z1);
+  const Fp S2 = fp_mul(fp_mul(y2, p.z), Z1Z1);
+  const Fp H = fp_reduce(fp_sub(U2, p.x));
+  const Fp rr = fp_reduce(fp_lin(2, S2, -2, p.y));
+  if (fp_is_zero(H)) {
+    if (fp_is_zero(rr)) return g1_dbl_lane(p);
+    return qj_inf();
+  }
+  const Fp HH = fp_sqr(H);
+  const Fp I = fp_lin(4, HH, 0, HH);
+  const Fp J = fp_mul(H, I);
+  const Fp V = fp_mul(p.x, I);
+  QJ r;
+  r.x = fp_reduce(fp_sub(fp_sub(fp_sqr(rr), J), fp_add(V, V)));
+  const Fp YJ = fp_mul(p.y, J);
+  r.y = fp_reduce(fp_sub(fp_mul(rr, fp_sub(V, r.x)), fp_add(YJ, YJ)));
+  const Fp ZH = fp_mul(p.z, H);
+  r.z = fp_reduce(fp_add(ZH, ZH));
+  return r;
+}
+
+// thread k of quad-group checks ack order[k] (order may be null)
+__global__ void __launch_bounds__(256) k_bivar_check_quad(int nack, int t, const uint32_t* __restrict__ rows,
+                                                          const uint32_t* __restrict__ row_idx,
+                                                          const uint32_t* __restrict__ ys,
+                                                          const uint32_t* __restrict__ vals,
+                                                          const uint32_t* __restrict__ fbtab,
+                                                          const uint32_t* __restrict__ order,
+                                                          uint8_t* __restrict__ verdict) {
+  const int k = (int)((blockIdx.x * 256u + threadIdx.x) >> 2);
+  if (k >= nack) return;  // the four lanes of a quad leave together
+  const int a = order ? (int)order[k] : k;
+  const uint32_t* R = rows + (size_t)row_idx[a] * (t + 1) * Q_G1_WORDS;
+  const uint32_t y = ys[a];
+  // sum_j R_j y^j by Horner
+  QJ acc = qj_inf();
+#pragma unroll 1
+  for (int j = t; j >= 0; j--) {
+    acc = g1q_mul_small(acc, y);
+    Fp rx, ry;
+    if (!load_aff(R + (size_t)j * Q_G1_WORDS, rx, ry)) acc = g1q_add_affine(acc, rx, ry);
+  }
+  // g1 * val: lane q adds comb windows q, q + 4, ..., then the quad joins the four partial sums
+  const int q = q_lane();
+  QJ part = qj_inf();
+#pragma unroll 1
+  for (int w = q; w < Q_FB_WINDOWS; w += 4) {
+    const uint32_t d = (vals[(size_t)a * 8 + (w >> 2)] >> (8 * (w & 3))) & 0xffu;
+    if (d == 0) continue;
+    Fp x, yy;
+    if (!load_aff(fbtab + ((size_t)w * Q_FB_ROW + d) * Q_G1_WORDS, x, yy)) part = g1_madd_lane(part, x, yy);
+  }
+  QJ p0{q_dpp<0x00>(part.x), q_dpp<0x00>(part.y), q_dpp<0x00>(part.z)};
+  QJ p1{q_dpp<0x55>(part.x), q_dpp<0x55>(part.y), q_dpp<0x55>(part.z)};
+  QJ p2{q_dpp<0xAA>(part.x), q_dpp<0xAA>(part.y), q_dpp<0xAA>(part.z)};
+  QJ p3{q_dpp<0xFF>(part.x), q_dpp<0xFF>(part.y), q_dpp<0xFF>(part.z)};
+  const QJ w = g1q_add(g1q_add(p0, p1), g1q_add(p2, p3));
+  const bool ok = g1q_eq(acc, w);
+  if (q == 0) verdict[a] = ok ? 1 : 0;
+}
+
+}  // namespace hbs
+
+namespace hbl {
+
+hipError_t bivar_check_quad(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx,
+                            const uint32_t* ys, const uint32_t* vals, const void* fbtab, uint8_t* verdict,
+                            const uint32_t* order) {
+  if (nack <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hbs::k_bivar_check_quad, dim3((unsigned)((4 * (size_t)nack + 255) / 256)), dim3(256), 0, s, nack, t,
+                     (const uint32_t*)rows, row_idx, ys, vals, (const uint32_t*)fbtab, order, verdict);
+  return hipGetLastError();
+}
+
+}  // namespace hbl

@@ -87,8 +87,13 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
 // BivarCommitment::evaluate(x, y) == g1 * val for nack checks, given the rows R = row(x) of each
 // check's part: verdict[a] = (sum_j R[row_idx[a]][j] * y^j == g1 * val[a]).
 // fbtab: the fixed-base comb table of g1 (fb_table), used for the g1 * val side.
+// The same verdicts on lane quads (k_g1quad.hip): four lanes per ack split each point operation.
+hipError_t bivar_check_quad(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx,
+                            const uint32_t* ys, const uint32_t* vals, const void* fbtab, uint8_t* verdict,
+                            const uint32_t* order);
+// order (may be null): thread k checks ack order[k] (acks sorted by y keep a wave's lanes in step).
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
-                       const uint32_t* vals, const void* fbtab, uint8_t* verdict);
+                       const uint32_t* vals, const void* fbtab, uint8_t* verdict, const uint32_t* order = nullptr);
 // Fixed-base comb table of the G1 generator (32 windows x 256 affine points, fb_table_bytes()) and
 // out[i] = g1 * k_i from it (32 mixed additions per scalar).
 size_t fb_table_bytes();
