@@ -649,8 +649,8 @@ def run_dkg(args, eng, world, rank, dev):
         nack = len(vals)
         ops = [workcount.bivar_ack(t, y) for y in ys]
         op = (sum(o[0] for o in ops) / nack, sum(o[1] for o in ops) / nack)
-        main_k = roofline_entry("hb::k_bivar_row + hb::k_bivar_check", dev_n, dev_ms, nack, op, "ack check",
-                                nack / 64 / 1024)
+        main_k = roofline_entry("hb::k_bivar_row + hbs::k_bivar_check_quad", dev_n, dev_ms, nack, op, "ack check",
+                                4 * nack / 64 / 1024)
         line = {
             "metric": "SyncKeyGen ack checks/sec (whole node set), N=100 t=33", "value": nack * world / (ms / 1e3),
             "unit": "acks/s", "n_gpus": world, "steps": nsteps, "warmup": 1, "ms_per_step": ms,
@@ -662,9 +662,9 @@ def run_dkg(args, eng, world, rank, dev):
                                  "the 5.7 MB commitment upload"},
             "host_to_host_ms": host_ms, "verdicts_ok": ok,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
-                             traffic=pmc_traffic("hb::k_bivar_check"),
-                             note="one thread per ack, 10,000 acks = 157 waves: latency-bound at this size "
-                                  "(0.15 waves per SIMD)"),
+                             traffic=pmc_traffic("hbs::k_bivar_check_quad"),
+                             note="four lanes per ack (lane quads), 10,000 acks = 625 waves: latency-bound at "
+                                  "this size (0.6 waves per SIMD)"),
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, g1)
