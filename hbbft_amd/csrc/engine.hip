@@ -1036,7 +1036,7 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   HBH_CHECK(e->in_a.ensure(nparts * ncoef * HBH_G1_BYTES));
   HBH_CHECK(e->in_b.ensure(nrow * 8 + nack * 12));
   HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
-  HBH_CHECK(e->work.ensure(nrow * (t + 1) * HBH_G1_BYTES));
+  HBH_CHECK(e->work.ensure(hbl::bivar_rows_quad_bytes((int)nrow, t)));
   HBH_CHECK(e->out_v.ensure(nack));
   uint32_t* d_rp = (uint32_t*)e->in_b.p;
   uint32_t* d_rx = d_rp + nrow;
@@ -1051,7 +1051,7 @@ int hbh_bivar_ack_check(hbh_engine* e, size_t nack, int t, size_t nparts, const 
   HBH_CHECK(hipMemcpyAsync(d_ord, order.data(), nack * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, e->in_a.p, d_rp, d_rx, e->work.p));
+  HBH_CHECK(hbl::bivar_row_quad(s, (int)nrow, t, e->in_a.p, d_rp, d_rx, e->work.p));
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
   HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, e->work.p, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
@@ -1157,9 +1157,9 @@ int hbh_bivar_ack_check_dev(hbh_engine* e, void* stream, size_t nack, int t, con
   hipStream_t s = dev_stream(e, stream);
   rc = begin_call(e, s);
   if (rc) return rc;
-  HBH_CHECK(e->work.ensure(nrow * (t + 1) * HBH_G1_BYTES));
+  HBH_CHECK(e->work.ensure(hbl::bivar_rows_quad_bytes((int)nrow, t)));
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, d_commits, d_row_part, d_row_x, e->work.p));
+  HBH_CHECK(hbl::bivar_row_quad(s, (int)nrow, t, d_commits, d_row_part, d_row_x, e->work.p));
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
   HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, e->work.p, d_row_of, d_ys, (const uint32_t*)d_vals, e->fbtab.p,

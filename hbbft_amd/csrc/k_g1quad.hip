@@ -7,8 +7,9 @@
 // length is the time.  Here four lanes hold the same point and split every group operation's
 // independent Fp products between them, one product per lane per round, exchanging results with DPP
 // quad broadcasts: a doubling takes 3 rounds instead of 7 serial products, a mixed or general
-// addition 5 instead of 11 / 16.  g1 * val: each lane adds its quarter of the 32 comb windows on its
-// own, then the quad joins the four partial sums.  Formulas: dbl-2009-l, madd-2007-bl, add-2007-bl
+// addition 5 instead of 11 / 16.  The rows R = row(x) come from k_bivar_row_quad in Jacobian form
+// (no inversion per row element).  g1 * val: each lane adds its quarter of the 32 comb windows on
+// its own, then the quad joins the four partial sums.  Formulas: dbl-2009-l, madd-2007-bl, add-2007-bl
 // (the group law of curve.hpp) on the signed-limb Fp of sfp.hpp; the verdict is point equality, so
 // it is the one of k_bivar_check.
 #include "launch.hpp"
@@ -197,7 +198,53 @@ __device__ __forceinline__ QJ g1_madd_lane(const QJ& p, const Fp& x2, const Fp& 
   return r;
 }
 
-// thread k of quad-group checks ack order[k] (order may be null)
+// Jacobian row points in the engine's workspace: 3 x 14 signed limbs (Montgomery), z = 0 at infinity
+constexpr int Q_JROW_WORDS = 3 * NL;
+__device__ __forceinline__ void qj_store(int32_t* __restrict__ o, const QJ& p) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    o[i] = p.x.l[i];
+    o[NL + i] = p.y.l[i];
+    o[2 * NL + i] = p.z.l[i];
+  }
+}
+__device__ __forceinline__ QJ qj_load(const int32_t* __restrict__ o) {
+  QJ p;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    p.x.l[i] = o[i];
+    p.y.l[i] = o[NL + i];
+    p.z.l[i] = o[2 * NL + i];
+  }
+  return p;
+}
+__device__ __forceinline__ int q_coeff_pos(int i, int j) {  // BivarCommitment's symmetric index
+  return i <= j ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j;
+}
+
+// BivarCommitment::row(x)[i] = sum_j C[coeff_pos(i, j)] x^j (src/sync_key_gen.rs:496) by Horner
+// with the small x, one quad per (row, i); the result stays Jacobian (no inversion): the ack check
+// adds it with the general addition, which costs the quad the same 5 rounds as a mixed one.
+__global__ void __launch_bounds__(256) k_bivar_row_quad(int nrow, int t, const uint32_t* __restrict__ commits,
+                                                        const uint32_t* __restrict__ part_idx,
+                                                        const uint32_t* __restrict__ xs, int32_t* __restrict__ out) {
+  const int g = (int)((blockIdx.x * 256u + threadIdx.x) >> 2);
+  if (g >= nrow * (t + 1)) return;
+  const int r = g / (t + 1), i = g % (t + 1);
+  const int ncoef = (t + 1) * (t + 2) / 2;
+  const uint32_t* C = commits + (size_t)part_idx[r] * ncoef * Q_G1_WORDS;
+  const uint32_t x = xs[r];
+  QJ acc = qj_inf();
+#pragma unroll 1
+  for (int j = t; j >= 0; j--) {
+    acc = g1q_mul_small(acc, x);
+    Fp cx, cy;
+    if (!load_aff(C + (size_t)q_coeff_pos(i, j) * Q_G1_WORDS, cx, cy)) acc = g1q_add_affine(acc, cx, cy);
+  }
+  if (q_lane() == 0) qj_store(out + (size_t)g * Q_JROW_WORDS, acc);
+}
+
+// thread k of quad-group checks ack order[k] (order may be null); rows: Jacobian (k_bivar_row_quad)
 __global__ void __launch_bounds__(256) k_bivar_check_quad(int nack, int t, const uint32_t* __restrict__ rows,
                                                           const uint32_t* __restrict__ row_idx,
                                                           const uint32_t* __restrict__ ys,
@@ -208,15 +255,14 @@ __global__ void __launch_bounds__(256) k_bivar_check_quad(int nack, int t, const
   const int k = (int)((blockIdx.x * 256u + threadIdx.x) >> 2);
   if (k >= nack) return;  // the four lanes of a quad leave together
   const int a = order ? (int)order[k] : k;
-  const uint32_t* R = rows + (size_t)row_idx[a] * (t + 1) * Q_G1_WORDS;
+  const int32_t* R = (const int32_t*)rows + (size_t)row_idx[a] * (t + 1) * Q_JROW_WORDS;
   const uint32_t y = ys[a];
   // sum_j R_j y^j by Horner
   QJ acc = qj_inf();
 #pragma unroll 1
   for (int j = t; j >= 0; j--) {
     acc = g1q_mul_small(acc, y);
-    Fp rx, ry;
-    if (!load_aff(R + (size_t)j * Q_G1_WORDS, rx, ry)) acc = g1q_add_affine(acc, rx, ry);
+    acc = g1q_add(acc, qj_load(R + (size_t)j * Q_JROW_WORDS));
   }
   // g1 * val: lane q adds comb windows q, q + 4, ..., then the quad joins the four partial sums
   const int q = q_lane();
@@ -240,6 +286,17 @@ __global__ void __launch_bounds__(256) k_bivar_check_quad(int nack, int t, const
 }  // namespace hbs
 
 namespace hbl {
+
+size_t bivar_rows_quad_bytes(int nrow, int t) { return (size_t)nrow * (t + 1) * hbs::Q_JROW_WORDS * 4; }
+
+hipError_t bivar_row_quad(hipStream_t s, int nrow, int t, const void* commits, const uint32_t* part_idx,
+                          const uint32_t* xs, void* rows) {
+  if (nrow <= 0) return hipSuccess;
+  const size_t lanes = 4 * (size_t)nrow * (t + 1);
+  hipLaunchKernelGGL(hbs::k_bivar_row_quad, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, nrow, t,
+                     (const uint32_t*)commits, part_idx, xs, (int32_t*)rows);
+  return hipGetLastError();
+}
 
 hipError_t bivar_check_quad(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx,
                             const uint32_t* ys, const uint32_t* vals, const void* fbtab, uint8_t* verdict,

@@ -88,6 +88,10 @@ hipError_t bivar_row(hipStream_t s, int nrow, int t, const void* commits, const 
 // check's part: verdict[a] = (sum_j R[row_idx[a]][j] * y^j == g1 * val[a]).
 // fbtab: the fixed-base comb table of g1 (fb_table), used for the g1 * val side.
 // The same verdicts on lane quads (k_g1quad.hip): four lanes per ack split each point operation.
+// Rows from bivar_row_quad: Jacobian signed-limb points, bivar_rows_quad_bytes(nrow, t) of scratch.
+size_t bivar_rows_quad_bytes(int nrow, int t);
+hipError_t bivar_row_quad(hipStream_t s, int nrow, int t, const void* commits, const uint32_t* part_idx,
+                          const uint32_t* xs, void* rows);
 hipError_t bivar_check_quad(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx,
                             const uint32_t* ys, const uint32_t* vals, const void* fbtab, uint8_t* verdict,
                             const uint32_t* order);
