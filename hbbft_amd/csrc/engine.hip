@@ -635,7 +635,31 @@ void hfr_to_canon(const HFr& a, uint64_t* out) {
 
 // k_interp_digits on the host: the four GLS digits (base |x|) of every lambda_k(0) of each combine;
 // status[c] = HBH_ERR_DUPLICATE_ENTRY and zero digits on a repeated x
-void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* digits, int* status) {
+// q (4 x u64) <- q / x^2, rem <- q mod x^2 (bit-serial, the host twin of k_curve.hip div_x2)
+void host_div_x2(uint64_t q[4], uint64_t rem[2]) {
+  constexpr uint64_t X2_LO = 0x0000000100000000ull, X2_HI = 0xac45a4010001a402ull;
+  uint64_t r0 = 0, r1 = 0;
+  for (int w = 3; w >= 0; w--) {
+    uint64_t qw = 0;
+    for (int b = 63; b >= 0; b--) {
+      const bool top = (r1 >> 63) != 0;
+      r1 = (r1 << 1) | (r0 >> 63);
+      r0 = (r0 << 1) | ((q[w] >> b) & 1);
+      const bool ge = top || r1 > X2_HI || (r1 == X2_HI && r0 >= X2_LO);
+      if (ge) {
+        const uint64_t nr0 = r0 - X2_LO;
+        r1 = r1 - X2_HI - (r0 < X2_LO ? 1 : 0);
+        r0 = nr0;
+      }
+      qw |= (uint64_t)ge << b;
+    }
+    q[w] = qw;
+  }
+  rem[0] = r0;
+  rem[1] = r1;
+}
+
+void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* digits, int* status, bool g1 = false) {
   constexpr uint64_t XA = 0xd201000000010000ull;
   std::vector<HFr> x(m), num(m), den(m), pre(m);
   for (size_t c = 0; c < ncomb; c++) {
@@ -667,6 +691,15 @@ void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* di
       if (k) inv = hfr_mul(inv, den[k]);
       uint64_t q[4];
       hfr_to_canon(hfr_mul(num[k], ik), q);
+      if (g1) {  // lambda = d0 + d1 x^2
+        uint64_t rem[2];
+        host_div_x2(q, rem);
+        dg[k * 4 + 0] = rem[0];
+        dg[k * 4 + 1] = rem[1];
+        dg[k * 4 + 2] = q[0];
+        dg[k * 4 + 3] = q[1];
+        continue;
+      }
       for (int j = 0; j < 3; j++) {  // q <- q / |x|, digit j = remainder
         u128 rem = 0;
         for (int w = 3; w >= 0; w--) {
@@ -711,6 +744,32 @@ int launch_combine_g2(hbh_engine* e, hipStream_t s, size_t ncomb, size_t m, cons
   return HBH_OK;
 }
 
+// G1 combines: few combines take the lane-quad latency form (digits + k_interp_g1q + join), many
+// k_interp_endo<Fp> (throughput form).
+#ifndef HBH_INTERP_G1Q_MAX
+#define HBH_INTERP_G1Q_MAX 256  // quad form: 1 combine 0.91 ms, 100 1.74 ms (k_interp_endo<Fp>: 3.2 ms), 256 3.0 ms; 1,024 endo 4.1 ms
+#endif
+int launch_combine_g1(hbh_engine* e, hipStream_t s, size_t ncomb, size_t m, const uint32_t* d_xs, const void* d_pts,
+                      void* d_out, int* d_status, const uint32_t* h_xs = nullptr) {
+  if (ncomb <= HBH_INTERP_G1Q_MAX && m <= 4096) {
+    HBH_CHECK(e->in_d.ensure(ncomb * m * 4 * sizeof(uint64_t)));
+    if (h_xs && ncomb <= HOST_DIGITS_MAX) {
+      e->h_digits.resize(ncomb * m * 4);
+      e->h_status.resize(ncomb);
+      host_interp_digits(h_xs, ncomb, m, e->h_digits.data(), e->h_status.data(), true);
+      HBH_CHECK(hipMemcpyAsync(e->in_d.p, e->h_digits.data(), ncomb * m * 32, hipMemcpyHostToDevice, s));
+      HBH_CHECK(hipMemcpyAsync(d_status, e->h_status.data(), ncomb * sizeof(int), hipMemcpyHostToDevice, s));
+    } else {
+      HBH_CHECK(hbl::interp_digits(s, (int)ncomb, (int)m, d_xs, (uint64_t*)e->in_d.p, d_status, true));
+    }
+    HBH_CHECK(e->ipart.ensure(hbl::interp_g1_quad_part_bytes((int)ncomb)));
+    HBH_CHECK(hbl::interp_g1_quad(s, (int)ncomb, (int)m, (const uint64_t*)e->in_d.p, d_pts, e->ipart.p, d_out));
+    return HBH_OK;
+  }
+  HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, d_xs, d_pts, d_out, d_status));
+  return HBH_OK;
+}
+
 int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const uint8_t* pts, uint8_t* out, int* status,
                bool g2) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
@@ -746,8 +805,9 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
                            xs.data());
     if (rc) return rc;
   } else {
-    HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p,
-                              (int*)e->status.p));
+    rc = launch_combine_g1(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
+                           xs.data());
+    if (rc) return rc;
   }
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * pb, hipMemcpyDeviceToHost, s));
@@ -1095,8 +1155,10 @@ int run_interp_dev(hbh_engine* e, void* stream, size_t ncomb, int t, const uint3
   if (g2) {
     rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status);
     if (rc) return rc;
-  } else
-    HBH_CHECK(hbl::combine_g1(s, (int)ncomb, (int)m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status));
+  } else {
+    rc = launch_combine_g1(e, s, ncomb, m, (const uint32_t*)e->in_a.p, d_pts, d_out, d_status);
+    if (rc) return rc;
+  }
   e->timer.end(s, tm);
   return end_call(e, s);
 }

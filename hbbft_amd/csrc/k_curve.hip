@@ -367,8 +367,9 @@ __global__ void __launch_bounds__(256) k_interp_endo(int ncomb, int m, const uin
 // Stage 1 of the latency form of the G2 combine (k_interp_pair.hip does the curve work): the four
 // 64-bit GLS digits of every lambda_k(0) (the endo_term split), digits[(c*m + k)*4 + j].  One
 // workgroup per combine; a duplicate x sets status[c] = HBL_DUPLICATE and zero digits (terms = O).
+// g1: the two 128-bit GLV digits instead (d[0..1] = lambda mod x^2, d[2..3] = lambda div x^2, low word first).
 __global__ void __launch_bounds__(64) k_interp_digits(int ncomb, int m, const uint32_t* __restrict__ xs,
-                                                      uint64_t* __restrict__ digits, int* __restrict__ status) {
+                                                      uint64_t* __restrict__ digits, int* __restrict__ status, int g1) {
   extern __shared__ unsigned char smem_raw[];
   __shared__ int s_dup;
   Fr* snum = reinterpret_cast<Fr*>(smem_raw);
@@ -408,10 +409,19 @@ __global__ void __launch_bounds__(64) k_interp_digits(int ncomb, int m, const ui
     uint64_t q[4];
     k_to_u64(slam[k].l, q);
     uint64_t* d = digits + ((size_t)c * m + k) * 4;
-    d[0] = div_x_abs(q);
-    d[1] = div_x_abs(q);
-    d[2] = div_x_abs(q);
-    d[3] = q[0];
+    if (g1) {
+      uint64_t rem[2];
+      div_x2(q, rem);
+      d[0] = rem[0];
+      d[1] = rem[1];
+      d[2] = q[0];
+      d[3] = q[1];
+    } else {
+      d[0] = div_x_abs(q);
+      d[1] = div_x_abs(q);
+      d[2] = div_x_abs(q);
+      d[3] = q[0];
+    }
   }
 }
 
@@ -578,10 +588,10 @@ hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint
   return hipGetLastError();
 }
 
-hipError_t interp_digits(hipStream_t s, int ncomb, int m, const uint32_t* xs, uint64_t* digits, int* status) {
+hipError_t interp_digits(hipStream_t s, int ncomb, int m, const uint32_t* xs, uint64_t* digits, int* status, bool g1) {
   if (ncomb <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_interp_digits, dim3((unsigned)ncomb), dim3(64), (size_t)3 * m * sizeof(hb::Fr), s, ncomb, m,
-                     xs, digits, status);
+                     xs, digits, status, g1 ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -12,8 +12,10 @@
 // its own, then the quad joins the four partial sums.  Formulas: dbl-2009-l, madd-2007-bl, add-2007-bl
 // (the group law of curve.hpp) on the signed-limb Fp of sfp.hpp; the verdict is point equality, so
 // it is the one of k_bivar_check.
+#include "interp_pair.hpp"
 #include "launch.hpp"
 #include "sfp.hpp"
+#include "words.hpp"
 
 namespace hbs {
 
@@ -283,9 +285,113 @@ __global__ void __launch_bounds__(256) k_bivar_check_quad(int nack, int t, const
   if (q == 0) verdict[a] = ok ? 1 : 0;
 }
 
+// ---------------------------------------------------------------- G1 Lagrange combine, latency form
+// PublicKeySet::decrypt's interpolation (src/threshold_decrypt.rs:242-250) for a few ciphertexts: the
+// GLV split lambda = d0 + d1 x^2 (phi(x, y) = (beta x, y) = [-x^2], so x^2 P = (beta x, -y)), each
+// 128-bit digit in four 32-bit chunks; workgroup (c, s) sums chunk s of every term on 64 lane quads,
+// an LDS tree joins them and quad 0 shifts the sum by 2^(32 s) (Horner); k_interp_g1_join adds the four
+// partial sums and writes the affine point.  The group law of curve.hpp, so the affine bytes equal
+// k_interp_endo<Fp>'s and the C oracle's.
+constexpr int G1Q_NCHUNK = 4;
+constexpr int G1Q_Q = 64;  // quads per workgroup
+
+__device__ __forceinline__ QJ g1q_mul_affine(const Fp& x, const Fp& y, bool inf, uint32_t k) {
+  if (inf || k == 0) return qj_inf();
+  const int top = 31 - __builtin_clz(k);
+  QJ acc{x, y, fp_one()};
+#pragma unroll 1
+  for (int i = top - 1; i >= 0; i--) {
+    acc = g1q_dbl(acc);
+    if ((k >> i) & 1) acc = g1q_add_affine(acc, x, y);
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) k_interp_g1q(int ncomb, int m, const uint64_t* __restrict__ digits,
+                                                    const uint32_t* __restrict__ pts, int32_t* __restrict__ part) {
+  __shared__ int32_t sm[G1Q_Q * Q_JROW_WORDS];
+  const int c = blockIdx.x / G1Q_NCHUNK, chunk = blockIdx.x % G1Q_NCHUNK;
+  if (c >= ncomb) return;  // uniform per workgroup
+  const int g = threadIdx.x >> 2;
+  QJ acc = qj_inf();
+  for (int t = g; t < m * 2; t += G1Q_Q) {
+    const int k = t >> 1, j = t & 1;
+    Fp x, y;
+    const bool inf = load_aff(pts + ((size_t)c * m + k) * Q_G1_WORDS, x, y);
+    if (j) {
+      x = fp_reduce(fp_mul(x, fp_const(hb::BETA_M)));
+      y = fp_neg(y);
+    }
+    const uint64_t d = digits[((size_t)c * m + k) * 4 + 2 * j + (chunk >> 1)];
+    const uint32_t kc = (uint32_t)(d >> (32 * (chunk & 1)));
+    acc = g1q_add(acc, g1q_mul_affine(x, y, inf, kc));
+  }
+  if (q_lane() == 0) qj_store(sm + g * Q_JROW_WORDS, acc);
+  __syncthreads();
+  for (int s = G1Q_Q / 2; s > 0; s >>= 1) {
+    if (g < s) acc = g1q_add(qj_load(sm + g * Q_JROW_WORDS), qj_load(sm + (g + s) * Q_JROW_WORDS));
+    __syncthreads();
+    if (g < s && q_lane() == 0) qj_store(sm + g * Q_JROW_WORDS, acc);
+    __syncthreads();
+  }
+  if (g != 0) return;
+  QJ r = qj_load(sm);
+#pragma unroll 1
+  for (int b = 0; b < 32 * chunk; b++) r = g1q_dbl(r);
+  if (q_lane() == 0) qj_store(part + (size_t)blockIdx.x * Q_JROW_WORDS, r);
+}
+
+__device__ __forceinline__ Fp fp_inv_vartime(const Fp& a) {
+  uint32_t w[12], p[12], r[12];
+  fp_to_words(a, w);
+#pragma unroll
+  for (int i = 0; i < 12; i++) p[i] = hb::PM2_W[i];
+  p[0] += 2;  // p - 2 + 2
+  hb::words_inv_vartime<12>(w, p, r);
+  return fp_from_words(r);
+}
+
+// out[c] = affine(sum of the four chunk sums), one lane quad per combine
+__global__ void __launch_bounds__(64) k_interp_g1_join(int ncomb, const int32_t* __restrict__ part,
+                                                       uint32_t* __restrict__ out) {
+  const int c = (int)((blockIdx.x * 64u + threadIdx.x) >> 2);
+  if (c >= ncomb) return;
+  const int32_t* p = part + (size_t)c * G1Q_NCHUNK * Q_JROW_WORDS;
+  const QJ r = g1q_add(g1q_add(qj_load(p), qj_load(p + Q_JROW_WORDS)),
+                       g1q_add(qj_load(p + 2 * Q_JROW_WORDS), qj_load(p + 3 * Q_JROW_WORDS)));
+  uint32_t* o = out + (size_t)c * Q_G1_WORDS;
+  if (qj_zero(r)) {
+    if (q_lane() == 0)
+      for (int i = 0; i < Q_G1_WORDS; i++) o[i] = 0u;
+    return;
+  }
+  const Fp zi = fp_inv_vartime(fp_reduce(r.z));
+  Fp zi2, u, xa, ya;
+  zi2 = fp_sqr(zi);
+  q2(r.x, zi2, zi2, zi, xa, u);
+  ya = fp_mul(r.y, u);
+  if (q_lane() == 0) {
+    fp_to_words(xa, o);
+    fp_to_words(ya, o + 12);
+  }
+}
+
 }  // namespace hbs
 
 namespace hbl {
+
+size_t interp_g1_quad_part_bytes(int ncomb) { return (size_t)ncomb * hbs::G1Q_NCHUNK * hbs::Q_JROW_WORDS * 4; }
+
+hipError_t interp_g1_quad(hipStream_t s, int ncomb, int m, const uint64_t* digits, const void* pts, void* part,
+                          void* out) {
+  if (ncomb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hbs::k_interp_g1q, dim3((unsigned)ncomb * hbs::G1Q_NCHUNK), dim3(256), 0, s, ncomb, m, digits,
+                     (const uint32_t*)pts, (int32_t*)part);
+  hipLaunchKernelGGL(hbs::k_interp_g1_join, dim3((unsigned)((4 * ncomb + 63) / 64)), dim3(64), 0, s, ncomb,
+                     (const int32_t*)part, (uint32_t*)out);
+  return hipGetLastError();
+}
+
 
 size_t bivar_rows_quad_bytes(int nrow, int t) { return (size_t)nrow * (t + 1) * hbs::Q_JROW_WORDS * 4; }
 
