@@ -42,10 +42,11 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
-IMPLS = {"lane_coop": 1, "thread_signed": 2, "auto": 3, "pair": 4}   # HBH_IMPL_* (include/hbbft_hip.h)
+IMPLS = {"lane_coop": 1, "thread_signed": 2, "auto": 3, "pair": 4, "wave": 5}   # HBH_IMPL_* (include/hbbft_hip.h)
 KERNEL_NAMES = {"lane_coop": "hbs::k_lc_* (miller+easy+exp+glue+verdict)",
                 "thread_signed": "hbs::k_ts_* (miller+easy+exp+glue+verdict)",
                 "pair": "hbs::k_pair_verify<false, true, 2>",
+                "wave": "hbs::k_wave (one wave per check)",
                 "auto": "hbs::k_pair_verify<false, true, 2>"}
 G1_UNC = bytes.fromhex(
     "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
@@ -323,7 +324,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
-    ap.add_argument("--impl", choices=["lane_coop", "thread_signed", "pair", "auto"], default="auto",
+    ap.add_argument("--impl", choices=["lane_coop", "thread_signed", "pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
     ap.add_argument("--workload", choices=["sign", "decrypt", "dkg", "epoch"], default="sign",
@@ -729,7 +730,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
         drained = sum(r.checks_gpu for r in results)
         consumed = sum(r.checks_consumed for r in results) / len(results)
         phases = {k: sum(r.timing[k] for r in results) / len(results) * 1e3 for k in results[0].timing}
-        main_k = roofline_entry("hbs::k_pair_verify", pair_n, pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
+        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX checks (all of an epoch's) to the wave kernel.
+        main_k = roofline_entry("hbs::k_wave", pair_n, pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
                                 workcount.PAIR_CHECK_WALK, "share / ciphertext check")
         line = {
             "metric": "HoneyBadger epochs/sec, one node's threshold crypto, N=100 f=33", "value": world * 1e3 / ms,
