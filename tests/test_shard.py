@@ -89,3 +89,31 @@ def test_shard_by_instance_golden_batch_gloo(world):
     spans = sorted(sp[0] for _, sp in got)
     assert spans == [(0, 10), (10, 20)]  # one document per rank, never split
     assert out == bytes(int(v) for _, _, _, v in items)
+
+
+def _max_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["HBH_DIST_BACKEND"] = "gloo"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    got = bench._max_over_ranks(10.0 + rank * 3.5, world, None)
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_bench_step_time_is_max_over_ranks_gloo(world):
+    """bench.py's multi-rank timing: every rank gets the slowest rank's step time (the value the
+    JSON line divides the job's units by)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_max_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == {r: 10.0 + (world - 1) * 3.5 for r in range(world)}
