@@ -161,6 +161,54 @@ HP_D Fp h_inv_vartime(const Fp& a) {
   return h_conj(fp_mul(a, fp_from_words(r)));
 }
 
+// ---------------------------------------------------------------- one-pass reductions
+// reduce(M t + K a) in one carry pass: t unnormalised limbs (|t_i| < 2^31), a normalised, |M|, |K|
+// <= 3.  The quotient comes from the top limb alone (as in fp_reduce); the lower limbs' excess moves
+// the value by < 2^368 < 2^-12 p, so the output is normalised and in (-p/1000, p + p/1000) --
+// inside (R).  Replaces a normalisation pass per sum plus fp_reduce's pass.
+template <int M, int K>
+HP_D Fp fp_red_mk(const Fp& t, const Fp& a) {
+  const int64_t top = (int64_t)t.l[NL - 1] * M + (int64_t)K * a.l[NL - 1];
+  const int32_t q = (int32_t)((top * QINV) >> 32);
+  Fp r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    acc += (int64_t)t.l[i] * M + (int64_t)K * a.l[i] - (int64_t)q * (int32_t)P_L[i];
+    r.l[i] = (int32_t)acc & MASK28;
+    acc >>= 28;
+  }
+  r.l[NL - 1] = (int32_t)(acc + top - (int64_t)q * (int32_t)P_L[NL - 1]);
+  return r;
+}
+HP_D Fp fp_red_l(const Fp& t) { return fp_red_mk<1, 0>(t, t); }
+// own component of s + xi t without normalising (|s_i| + 2 |t_i| < 2^31)
+HP_D Fp h_add_xi_l(const Fp& s, const Fp& t) {
+  const int32_t sm = lp_even() ? -1 : 0;
+  const Fp pt = dpp_fp<DPP_SWAP>(t);
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = s.l[i] + t.l[i] + ((pt.l[i] ^ sm) - sm);
+  return r;
+}
+// a - b - c without normalising
+HP_D Fp fp_sub2l(const Fp& a, const Fp& b, const Fp& c) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = a.l[i] - b.l[i] - c.l[i];
+  return r;
+}
+
+// own component of xi t without normalising
+HP_D Fp h_xi_l(const Fp& t) {
+  const int32_t sm = lp_even() ? -1 : 0;
+  const Fp pt = dpp_fp<DPP_SWAP>(t);
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = t.l[i] + ((pt.l[i] ^ sm) - sm);
+  return r;
+}
+
 // ---------------------------------------------------------------- Fp6 / Fp12 (own components)
 struct H6 { Fp c0, c1, c2; };
 struct H12 { H6 c0, c1; };
@@ -173,18 +221,17 @@ HP_D H6 h6_neg(const H6& a) { return {fp_neg(a.c0), fp_neg(a.c1), fp_neg(a.c2)};
 HP_D H6 h6_red(const H6& a) { return {fp_reduce(a.c0), fp_reduce(a.c1), fp_reduce(a.c2)}; }
 HP_D H6 h6_mul_v(const H6& a) { return {h_mul_xi(a.c2), a.c0, a.c1}; }
 
-// Karatsuba (stower.hpp f6_mul), inputs < 4p
+// Karatsuba (stower.hpp f6_mul), inputs < 4p; outputs reduced (each one sum formed unnormalised
+// and reduced in one pass)
 HP_D H6 h6_mul(const H6& a, const H6& b) {
   const Fp v0 = h_mul(a.c0, b.c0);
   const Fp v1 = h_mul(a.c1, b.c1);
   const Fp v2 = h_mul(a.c2, b.c2);
-  Fp t0 = h_mul(fp_addl(a.c1, a.c2), fp_add(b.c1, b.c2));
-  Fp t1 = h_mul(fp_addl(a.c0, a.c1), fp_add(b.c0, b.c1));
-  Fp t2 = h_mul(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2));
-  t0 = fp_sub(fp_subl(t0, v1), v2);
-  t1 = fp_sub(fp_subl(t1, v0), v1);
-  t2 = fp_sub(fp_subl(t2, v0), v2);
-  return {fp_add(v0, h_mul_xi(t0)), fp_add(t1, h_mul_xi(v2)), fp_add(t2, v1)};
+  const Fp t0 = h_mul(fp_addl(a.c1, a.c2), fp_add(b.c1, b.c2));
+  const Fp t1 = h_mul(fp_addl(a.c0, a.c1), fp_add(b.c0, b.c1));
+  const Fp t2 = h_mul(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2));
+  return {fp_red_l(h_add_xi_l(v0, fp_sub2l(t0, v1, v2))), fp_red_l(h_add_xi_l(fp_sub2l(t1, v0, v1), v2)),
+          fp_red_l(fp_addl(fp_sub2l(t2, v0, v2), v1))};
 }
 // x (a + b v)
 HP_D H6 h6_mul_01(const H6& x, const Fp& a, const Fp& b) {
@@ -214,19 +261,29 @@ HP_D H6 h6_inv(const H6& a) {
 HP_D H12 h12_one() { return {h6_one(), h6_zero()}; }
 HP_D H12 h12_conj(const H12& a) { return {a.c0, h6_neg(a.c1)}; }
 HP_D H12 h12_red(const H12& a) { return {h6_red(a.c0), h6_red(a.c1)}; }
+// Karatsuba recombination (t0 + v t1, s - t0 - t1) of normalised Fp6 products, reduced in one pass
+// per component
+HP_D H12 h12_kcomb(const H6& t0, const H6& t1, const H6& s) {
+  return {{fp_red_l(h_add_xi_l(t0.c0, t1.c2)), fp_red_l(fp_addl(t0.c1, t1.c0)), fp_red_l(fp_addl(t0.c2, t1.c1))},
+          {fp_red_l(fp_sub2l(s.c0, t0.c0, t1.c0)), fp_red_l(fp_sub2l(s.c1, t0.c1, t1.c1)),
+           fp_red_l(fp_sub2l(s.c2, t0.c2, t1.c2))}};
+}
 
 // inputs reduced; output reduced
 HP_D H12 h12_mul(const H12& a, const H12& b) {
   const H6 t0 = h6_mul(a.c0, b.c0);
   const H6 t1 = h6_mul(a.c1, b.c1);
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_add(b.c0, b.c1));
-  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
+  return h12_kcomb(t0, t1, s);
 }
 // complex squaring (stower.hpp f12_sqr)
 HP_D H12 h12_sqr(const H12& a) {
-  const H6 t = h6_red(h6_mul(a.c0, a.c1));
+  const H6 t = h6_mul(a.c0, a.c1);
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_red(h6_add(a.c0, h6_mul_v(a.c1))));
-  return h12_red({h6_sub(h6_sub(s, t), h6_mul_v(t)), h6_add(t, t)});
+  // (s - t - v t, 2 t)
+  return {{fp_red_l(fp_sub2l(s.c0, t.c0, h_xi_l(t.c2))), fp_red_l(fp_sub2l(s.c1, t.c1, t.c0)),
+           fp_red_l(fp_sub2l(s.c2, t.c2, t.c1))},
+          {fp_red_mk<2, 0>(t.c0, t.c0), fp_red_mk<2, 0>(t.c1, t.c1), fp_red_mk<2, 0>(t.c2, t.c2)}};
 }
 // f (c0 + c1 w^2 + c4 w^3); c0, c1, c4 normalised, < 2p
 HP_D H12 h12_mul_014(const H12& f, const Fp& c0, const Fp& c1, const Fp& c4) {
@@ -235,7 +292,7 @@ HP_D H12 h12_mul_014(const H12& f, const Fp& c0, const Fp& c1, const Fp& c4) {
   const H6 t0 = h6_red(h6_mul_01(f.c0, c0, c1));
   const H6 t1 = h6_red(h6_mul_1(f.c1, c4));
   const H6 s = h6_red(h6_mul_01(fs, c0, c14));
-  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
+  return h12_kcomb(t0, t1, s);
 }
 // x (b1 v + b2 v^2): c0 = xi (a1 b2 + a2 b1), c1 = a0 b1 + xi a2 b2, c2 = a0 b2 + a1 b1 (5 products)
 HP_D H6 h6_mul_12(const H6& x, const Fp& b1, const Fp& b2) {
@@ -259,13 +316,13 @@ HP_D H12 h12_mul_lines(const H12& f, const Fp& a0, const Fp& a1, const Fp& a4, c
   const Fp y2 = fp_sub(fp_subl(h_mul(fp_addl(a1, a4), fp_add(b1, b4)), a1b1), a4b4);
   const H6 C0 = h6_red({fp_add(a0b0, h_mul_xi(a4b4)), x1, a1b1});
   const Fp c11 = fp_reduce(y1), c12 = fp_reduce(y2);
-  const H6 t0 = h6_red(h6_mul(f.c0, C0));
+  const H6 t0 = h6_mul(f.c0, C0);
   const H6 t1 = h6_red(h6_mul_12(f.c1, c11, c12));
-  const H6 s = h6_red(h6_mul(h6_add(f.c0, f.c1), h6_red({C0.c0, fp_add(C0.c1, c11), fp_add(C0.c2, c12)})));
-  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
+  const H6 s = h6_mul(h6_add(f.c0, f.c1), h6_red({C0.c0, fp_add(C0.c1, c11), fp_add(C0.c2, c12)}));
+  return h12_kcomb(t0, t1, s);
 }
 HP_D H12 h12_inv(const H12& a) {
-  const H6 t = h6_red(h6_sub(h6_red(h6_mul(a.c0, a.c0)), h6_red(h6_mul_v(h6_red(h6_mul(a.c1, a.c1))))));
+  const H6 t = h6_red(h6_sub(h6_mul(a.c0, a.c0), h6_red(h6_mul_v(h6_mul(a.c1, a.c1)))));
   const H6 ti = h6_red(h6_inv(t));
   return h12_red({h6_mul(a.c0, ti), h6_neg(h6_mul(a.c1, ti))});
 }
@@ -292,30 +349,29 @@ HP_D H12 h12_frob2(const H12& f) {
   return r;
 }
 
-// Granger-Scott cyclotomic squaring (stower.hpp f12_cyclo_sqr), input reduced, output reduced
+// Granger-Scott cyclotomic squaring (stower.hpp f12_cyclo_sqr), input reduced, output reduced.
+// Each output 3 A -/+ 2 a is formed from the unnormalised squares and reduced in one carry pass
+// (fp_red_mk) instead of normalising A, the linear combination and the reduction separately.
 HP_D H12 h12_cyclo_sqr(const H12& f) {
   const Fp& a0 = f.c0.c0; const Fp& a2 = f.c0.c1; const Fp& a4 = f.c0.c2;
   const Fp& a1 = f.c1.c0; const Fp& a3 = f.c1.c1; const Fp& a5 = f.c1.c2;
   H12 r;
   {
     const Fp s0 = h_sqr(a0), s3 = h_sqr(a3), s03 = h_sqr(fp_add(a0, a3));
-    const Fp A0 = fp_add(s0, h_mul_xi(s3)), A1 = fp_sub(fp_subl(s03, s0), s3);
-    r.c0.c0 = fp_lin(3, A0, -2, a0);
-    r.c1.c1 = fp_lin(3, A1, 2, a3);
+    r.c0.c0 = fp_red_mk<3, -2>(h_add_xi_l(s0, s3), a0);
+    r.c1.c1 = fp_red_mk<3, 2>(fp_sub2l(s03, s0, s3), a3);
   }
   {
     const Fp s1 = h_sqr(a1), s4 = h_sqr(a4), s14 = h_sqr(fp_add(a1, a4));
-    const Fp B0 = fp_add(s1, h_mul_xi(s4)), B1 = fp_sub(fp_subl(s14, s1), s4);
-    r.c0.c1 = fp_lin(3, B0, -2, a2);
-    r.c1.c2 = fp_lin(3, B1, 2, a5);
+    r.c0.c1 = fp_red_mk<3, -2>(h_add_xi_l(s1, s4), a2);
+    r.c1.c2 = fp_red_mk<3, 2>(fp_sub2l(s14, s1, s4), a5);
   }
   {
     const Fp s2 = h_sqr(a2), s5 = h_sqr(a5), s25 = h_sqr(fp_add(a2, a5));
-    const Fp C0 = fp_add(s2, h_mul_xi(s5)), C1 = fp_sub(fp_subl(s25, s2), s5);
-    r.c1.c0 = fp_lin(3, h_mul_xi(C1), 2, a1);
-    r.c0.c2 = fp_lin(3, C0, -2, a4);
+    r.c0.c2 = fp_red_mk<3, -2>(h_add_xi_l(s2, s5), a4);
+    r.c1.c0 = fp_red_mk<3, 2>(h_xi_l(fp_sub2l(s25, s2, s5)), a1);
   }
-  return h12_red(r);
+  return r;
 }
 
 HP_D bool h12_is_one(const H12& f) {
