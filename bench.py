@@ -327,6 +327,8 @@ def main():
     ap.add_argument("--impl", choices=["lane_coop", "thread_signed", "pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="epoch workload: drain each window before handling it (no GPU/host overlap)")
     ap.add_argument("--workload", choices=["sign", "decrypt", "dkg", "epoch"], default="sign",
                     help="sign = BASELINE configs[1] (default, the headline metric); decrypt = configs[2] "
                          "(64k decryption-share checks + G1 combines, strong-scaled over ranks); dkg = configs[3] "
@@ -711,7 +713,7 @@ def run_epoch_bench(args, eng, world, rank, dev):
     log("generated %d epoch traces in %.1f s" % (len(traces), time.time() - t0))
     ok = True
     for tr in traces[:args.warmup]:
-        r = run_epoch(eng, keys, tr, window=args.window)
+        r = run_epoch(eng, keys, tr, window=args.window, pipelined=not args.no_pipeline)
         ok = ok and r.plaintexts == tr.proposals
     if world > 1:
         dist.barrier()
@@ -719,7 +721,7 @@ def run_epoch_bench(args, eng, world, rank, dev):
     eng.set_profiling(True)
     t0 = time.perf_counter()
     for tr in traces[args.warmup:]:
-        results.append(run_epoch(eng, keys, tr, window=args.window))
+        results.append(run_epoch(eng, keys, tr, window=args.window, pipelined=not args.no_pipeline))
     wall = time.perf_counter() - t0
     pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
     eng.set_profiling(False)
@@ -741,6 +743,7 @@ def run_epoch_bench(args, eng, world, rank, dev):
                     "1/64 forged shares); messages in random order",
             "config": {"workload": "HoneyBadger epoch crypto trace, BASELINE configs[4]", "n_nodes": n, "f": f,
                        "coins_per_epoch": len(traces[0].coin_docs), "window": args.window,
+                       "pipelined_drains": not args.no_pipeline,
                        "parallelism": "one node per rank x%d" % world,
                        "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},
             "outputs_ok": ok, "phase_ms": phases,

@@ -137,24 +137,53 @@ class EpochResult:
         self.combines = 0
 
 
-def _deliver(verifier, msgs, window, instance, queue, handle, res, kind):
+def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelined=True, limit=None):
     """Deliver msgs in windows: queue the checks of messages whose instance is still running,
-    drain once, then hand every message to its instance."""
-    for w0 in range(0, len(msgs), window):
-        batch = msgs[w0:w0 + window]
-        for p, j in batch:
-            if not instance[p].terminated:
-                queue(p, j)
-        verifier.drain()
+    drain once, then hand every message to its instance.
+
+    pipelined: window k's drain runs on the GPU (drain_async) while the host hands window k - 1's
+    messages to their instances; window k's checks are queued before window k - 1 is handled, so
+    an instance that terminates in window k - 1 may have a few checks drained that it never reads
+    (the verdicts, steps and faults are those of the serial order: verdicts are pure).
+
+    limit: pre-verify at most this many shares per instance (threshold + slack); a share the
+    instance still reads after that is a cache miss, verified on its own (BatchVerifier.*_valid)
+    -- same verdicts, fewer checks drained for instances that terminate early."""
+    def hand(batch):
         for p, j in batch:
             step = handle(p, j)
             res.faults += [(kind, p, f) for f in step.fault_log]
             if step.output:
                 yield p, step.output[0]
 
+    prev = None
+    queued = {}
+    for w0 in range(0, len(msgs), window):
+        batch = msgs[w0:w0 + window]
+        for p, j in batch:
+            if not instance[p].terminated:
+                c = queued.get(p, 0)
+                if limit is None or c < limit:
+                    queue(p, j)
+                    queued[p] = c + 1
+        if not pipelined:
+            verifier.drain()
+            yield from hand(batch)
+            continue
+        pending = verifier.drain_async()
+        if prev is not None:
+            yield from hand(prev)
+        verifier.commit(pending)
+        prev = batch
+    if prev is not None:
+        yield from hand(prev)
 
-def run_epoch(engine, keys, trace, window=4096, our=0, threads=0):
-    """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain."""
+
+def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True, slack=4):
+    """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
+    ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
+    ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share)."""
+    limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     ver = BatchVerifier(engine)
     ver.recording = True                   # combines of the epoch run in one batch at the end
@@ -184,7 +213,8 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0):
             coin_out[p] = step.output[0]
     for p, out in _deliver(ver, trace.coin_msgs, window, ts,
                            lambda p, j: ver.queue_sig(keys.pks[j], ts[p].doc_hash, trace.coin_shares[(p, j)]),
-                           lambda p, j: ts[p].handle_message(j, trace.coin_shares[(p, j)]), res, "coin"):
+                           lambda p, j: ts[p].handle_message(j, trace.coin_shares[(p, j)]), res, "coin", pipelined,
+                           limit):
         coin_out[p] = out
     res.timing["coin_verify"] = time.perf_counter() - t0
 
@@ -211,7 +241,8 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0):
             dec_out[p] = step.output[0]
     for p, out in _deliver(ver, trace.dec_msgs, window, td,
                            lambda p, j: ver.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], cts[p].huv, cts[p].w),
-                           lambda p, j: td[p].handle_message(j, trace.dec_shares[(p, j)]), res, "dec"):
+                           lambda p, j: td[p].handle_message(j, trace.dec_shares[(p, j)]), res, "dec", pipelined,
+                           limit):
         dec_out[p] = out
     res.timing["decrypt_verify"] = time.perf_counter() - t0
 

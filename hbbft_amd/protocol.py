@@ -14,6 +14,8 @@ What stays on the host, as in the reference and the north star: hashing to G2 (`
 ``decrypt_share_no_verify``: ``NetworkInfo`` holds callables) and the XOR stream of
 ``PublicKeySet::decrypt`` -- all through the product host stage (``hbbft_amd.hoststage``, C++).
 """
+import concurrent.futures
+
 from . import hoststage
 from ._lib import G1_BYTES, G2_BYTES
 
@@ -130,6 +132,8 @@ class BatchVerifier:
         self.lookups = 0        # verdicts the flows consumed (the checks the reference performs)
         self._docs = {}
         self._rec_g2, self._rec_g1 = [], []
+        self._released = set()  # instances released since the last drain was stored
+        self._inflight = 0      # drain_async calls not yet committed
 
     # -------------------------------------------------------------- host hashing
     def hash_docs(self, docs):
@@ -197,12 +201,14 @@ class BatchVerifier:
     def release_doc(self, h):
         """Drop the cached verdicts of a terminated ThresholdSign instance (document hash h)."""
         self._sig.pop(bytes(h), None)
+        self._released.add(bytes(h))
 
     def release_ct(self, huv, w):
         """Drop the cached verdicts of a terminated ThresholdDecrypt instance."""
         key = (bytes(huv), bytes(w))
         self._dec.pop(key, None)
         self._ct.pop(key, None)
+        self._released.add(key)
 
     def cached(self):
         return (sum(len(d) for d in self._sig.values()) + sum(len(d) for d in self._dec.values())
@@ -255,37 +261,84 @@ class BatchVerifier:
 
     def drain(self):
         """Verify everything queued: one engine call per kind."""
+        self._store(self._run_jobs(self._take_jobs()))
+
+    def drain_async(self):
+        """Start verifying everything queued on a worker thread (one engine call per kind, the
+        calls release the GIL) and return a handle for ``commit``.  Meanwhile the flows may handle
+        messages whose verdicts are already cached: a windowed driver overlaps the GPU drain of
+        window k with the host handling of window k - 1 (honey_badger._deliver)."""
+        global _POOL
+        jobs = self._take_jobs()
+        self._inflight += 1
+        if _POOL is None:
+            _POOL = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="hbh-drain")
+        return _POOL.submit(self._run_jobs, jobs)
+
+    def commit(self, pending):
+        """Wait for a ``drain_async`` and cache its verdicts."""
+        try:
+            res = pending.result()
+        finally:
+            self._inflight -= 1
+        self._store(res)
+
+    def _take_jobs(self):
+        """Snapshot the queues as engine-call arguments (main thread)."""
+        jobs = []
         if self._qct:
             keys = list(dict.fromkeys(self._qct))
             self._qct = []
-            v = self.eng.verify_ciphertexts([k[0] for k in keys], [k[1] for k in keys], [k[2] for k in keys])
-            self._count(len(keys))
-            for k, ok in zip(keys, v):
-                self._ct.setdefault((k[2], k[1]), {})[k[0]] = bool(ok)
+            jobs.append(("ct", keys, ([k[0] for k in keys], [k[1] for k in keys], [k[2] for k in keys])))
         if self._qsig:
             keys = list(dict.fromkeys(self._qsig))
             self._qsig = []
             hs = list(dict.fromkeys(k[1] for k in keys))
             hidx = {h: i for i, h in enumerate(hs)}
-            v = self.eng.verify_sig_shares([k[0] for k in keys], [k[2] for k in keys], hs, [hidx[k[1]] for k in keys])
-            self._count(len(keys))
-            for k, ok in zip(keys, v):
-                self._sig.setdefault(k[1], {})[(k[0], k[2])] = bool(ok)
+            jobs.append(("sig", keys, ([k[0] for k in keys], [k[2] for k in keys], hs, [hidx[k[1]] for k in keys])))
         if self._qdec:
             keys = list(dict.fromkeys(self._qdec))
             self._qdec = []
             cts = list(dict.fromkeys((k[2], k[3]) for k in keys))
             cidx = {c: i for i, c in enumerate(cts)}
-            v = self.eng.verify_dec_shares([k[1] for k in keys], [k[0] for k in keys], [c[0] for c in cts],
-                                           [c[1] for c in cts], [cidx[(k[2], k[3])] for k in keys])
+            jobs.append(("dec", keys, ([k[1] for k in keys], [k[0] for k in keys], [c[0] for c in cts],
+                                       [c[1] for c in cts], [cidx[(k[2], k[3])] for k in keys])))
+        return jobs
+
+    def _run_jobs(self, jobs):
+        """The engine calls of a snapshot (any thread): [(kind, keys, verdict bytes)]."""
+        fn = {"ct": self.eng.verify_ciphertexts, "sig": self.eng.verify_sig_shares, "dec": self.eng.verify_dec_shares}
+        return [(kind, keys, fn[kind](*args)) for kind, keys, args in jobs]
+
+    def _store(self, results):
+        """Cache verdicts (main thread).  Verdicts of instances released while their drain was in
+        flight are dropped, so a terminated instance leaves nothing behind."""
+        for kind, keys, v in results:
             self._count(len(keys))
-            for k, ok in zip(keys, v):
-                self._dec.setdefault((k[2], k[3]), {})[(k[0], k[1])] = bool(ok)
+            if kind == "ct":
+                for k, ok in zip(keys, v):
+                    if (k[2], k[1]) not in self._released:
+                        self._ct.setdefault((k[2], k[1]), {})[k[0]] = bool(ok)
+            elif kind == "sig":
+                for k, ok in zip(keys, v):
+                    if k[1] not in self._released:
+                        self._sig.setdefault(k[1], {})[(k[0], k[2])] = bool(ok)
+            else:
+                for k, ok in zip(keys, v):
+                    if (k[2], k[3]) not in self._released:
+                        self._dec.setdefault((k[2], k[3]), {})[(k[0], k[1])] = bool(ok)
+        # nothing queued after a release can name the released instance (the drivers queue only
+        # for running instances), so the set only has to outlive the drains in flight at release
+        if not self._inflight:
+            self._released.clear()
 
     def _count(self, n):
         self.calls += 1
         self.checks += n
         self.max_batch = max(self.max_batch, n)
+
+
+_POOL = None  # one worker thread for drain_async (engine calls are serialised per engine anyway)
 
 
 # ------------------------------------------------------------------ ThresholdSign (src/threshold_sign.rs)

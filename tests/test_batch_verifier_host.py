@@ -1,0 +1,74 @@
+"""BatchVerifier's drain bookkeeping on the CPU with a stand-in engine (no GPU): the synchronous
+drain and the pipelined drain_async/commit cache the same verdicts, every queued check reaches
+the engine once, and verdicts of an instance released while its drain was in flight are dropped
+(hbbft_amd/protocol.py; the windowed driver is hbbft_amd/honey_badger._deliver)."""
+import threading
+
+from hbbft_amd.protocol import BatchVerifier
+
+
+class FakeEngine:
+    """verdict = first byte of the share is even; records the thread of every call."""
+
+    def __init__(self):
+        self.calls = []
+
+    def verify_sig_shares(self, pks, sigs, hashes, doc_idx):
+        self.calls.append(("sig", len(pks), threading.current_thread().name))
+        return bytes(int(s[0] % 2 == 0) for s in sigs)
+
+    def verify_dec_shares(self, shares, pks, huv, w, ct_idx):
+        self.calls.append(("dec", len(shares), threading.current_thread().name))
+        return bytes(int(s[0] % 2 == 0) for s in shares)
+
+    def verify_ciphertexts(self, u, w, huv):
+        self.calls.append(("ct", len(u), threading.current_thread().name))
+        return bytes(1 for _ in u)
+
+
+def _fill(ver, docs=3, per=5):
+    items = []
+    for d in range(docs):
+        h = bytes([d]) * 8
+        for j in range(per):
+            pk, sh = bytes([j]) * 4, bytes([d * per + j]) * 4
+            ver.queue_sig(pk, h, sh)
+            items.append((pk, h, sh))
+    return items
+
+
+def test_sync_and_async_drains_cache_the_same_verdicts():
+    e1, e2 = FakeEngine(), FakeEngine()
+    v1, v2 = BatchVerifier(e1), BatchVerifier(e2)
+    items = _fill(v1)
+    _fill(v2)
+    v1.drain()
+    v2.commit(v2.drain_async())
+    for pk, h, sh in items:
+        assert v1.sig_valid(pk, h, sh) == v2.sig_valid(pk, h, sh) == (sh[0] % 2 == 0)
+    assert [c[:2] for c in e1.calls] == [c[:2] for c in e2.calls] == [("sig", 15)]
+    assert e2.calls[0][2].startswith("hbh-drain")
+    assert v2.checks == 15 and v2.calls == 1
+
+
+def test_release_during_async_drain_drops_verdicts():
+    eng = FakeEngine()
+    ver = BatchVerifier(eng)
+    _fill(ver, docs=2)
+    pending = ver.drain_async()
+    ver.release_doc(bytes([0]) * 8)      # instance 0 terminates while its drain is in flight
+    ver.commit(pending)
+    assert bytes([0]) * 8 not in ver._sig and bytes([1]) * 8 in ver._sig
+    assert ver.cached() == 5
+    assert not ver._released            # nothing in flight any more: the release set is empty
+
+
+def test_duplicates_are_checked_once():
+    eng = FakeEngine()
+    ver = BatchVerifier(eng)
+    _fill(ver, docs=1)
+    _fill(ver, docs=1)
+    ver.commit(ver.drain_async())
+    _fill(ver, docs=1)                   # already cached: nothing queued
+    ver.drain()
+    assert [c[:2] for c in eng.calls] == [("sig", 5)]

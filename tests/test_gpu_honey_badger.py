@@ -43,13 +43,20 @@ def test_epoch_small_and_window_equivalence(engine, n):
     trace = EpochTrace.generate(engine, keys, rng, hb_epoch=1, bad_every=5, proposal_bytes=100)
     big = run_epoch(engine, keys, trace, window=1 << 20)
     check(trace, big, keys)
-    one = run_epoch(engine, keys, trace, window=1)
+    one = run_epoch(engine, keys, trace, window=1, pipelined=False)
     check(trace, one, keys)
     assert (one.plaintexts, one.coins, one.signatures) == (big.plaintexts, big.coins, big.signatures)
     assert [(k, p, f.node_id, f.kind) for k, p, f in one.faults] == [(k, p, f.node_id, f.kind) for k, p, f in big.faults]
     # per-message verification checks exactly what the flows consume; the big window batches
     assert one.checks_gpu == one.checks_consumed
     assert big.engine_calls < one.engine_calls
+    # pipelined small windows (drain k on the GPU while window k - 1 is handled): same steps
+    for w in (1, 3):
+        pip = run_epoch(engine, keys, trace, window=w, pipelined=True)
+        check(trace, pip, keys)
+        assert (pip.plaintexts, pip.coins, pip.signatures) == (big.plaintexts, big.coins, big.signatures)
+        assert [(k, p, f.node_id, f.kind) for k, p, f in pip.faults] == [(k, p, f.node_id, f.kind) for k, p, f in big.faults]
+        assert pip.checks_gpu >= pip.checks_consumed
 
 
 def test_epoch_n100_f33(engine):
@@ -61,6 +68,9 @@ def test_epoch_n100_f33(engine):
     check(trace, res, keys)
     assert len(res.plaintexts) == 100 and len(res.coins) == 100
     assert res.engine_calls <= 16
+    ser = run_epoch(engine, keys, trace, window=4096, pipelined=False)
+    assert (ser.plaintexts, ser.coins, ser.signatures) == (res.plaintexts, res.coins, res.signatures)
+    assert [(k, p, f.node_id) for k, p, f in ser.faults] == [(k, p, f.node_id) for k, p, f in res.faults]
     print("epoch N=100: %.3f s, %d engine calls, %d checks drained, %d consumed, timing %s" % (
         res.timing["epoch"], res.engine_calls, res.checks_gpu, res.checks_consumed,
         {k: round(v, 4) for k, v in res.timing.items()}))
