@@ -16,8 +16,12 @@
 //   hash_g1_g2    hash_g2((V if |V| <= 64 else sha3(V)) || compress(U))
 //   xor_with_hash V xor low byte of successive next_u32 of ChaChaRng(sha3(compress(g)))
 //   parity        popcount of the XOR-fold of the 192-byte uncompressed G2 encoding, odd
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -324,10 +328,40 @@ static void xor_with_hash(const uint8_t* g_abi, const uint8_t* data, size_t len,
 }
 
 // ---------------------------------------------------------------- batching
-// run f(i) for i < n over `threads` workers (0 = all hardware threads)
+// CPUs this process may actually use: the affinity mask, capped by a cgroup v2 CPU quota
+// (cpu.max) and by OMP_NUM_THREADS / HBH_HOST_THREADS when set -- on a shared host
+// hardware_concurrency() counts the whole machine, and a thread per item beyond the quota only
+// adds creation cost and throttling.
+static size_t usable_cpus() {
+  static const size_t cached = [] {
+    size_t t = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) t = std::min(t, (size_t)std::max(1, CPU_COUNT(&set)));
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32] = {0};
+      long period = 0;
+      if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
+        const long q = std::atol(quota);
+        if (q > 0) t = std::min(t, (size_t)std::max(1L, (q + period - 1) / period));
+      }
+      std::fclose(f);
+    }
+    for (const char* env : {"HBH_HOST_THREADS", "OMP_NUM_THREADS"}) {
+      const char* v = std::getenv(env);
+      if (v && std::atoi(v) > 0) {
+        t = std::min(t, (size_t)std::atoi(v));
+        break;
+      }
+    }
+    return t;
+  }();
+  return cached;
+}
+
+// run f(i) for i < n over `threads` workers (0 = the usable CPUs)
 template <class F>
 static void parallel_for(size_t n, int threads, F f) {
-  size_t t = threads > 0 ? (size_t)threads : std::max(1u, std::thread::hardware_concurrency());
+  size_t t = threads > 0 ? (size_t)threads : usable_cpus();
   t = std::min(t, n);
   if (t <= 1) {
     for (size_t i = 0; i < n; i++) f(i);

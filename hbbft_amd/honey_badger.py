@@ -26,6 +26,7 @@ combines, timed on the C restatement by bench.py (oracle use stays in bench/test
 """
 import random
 import struct
+import sys
 import time
 
 from . import hoststage
@@ -156,8 +157,21 @@ def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelin
             if step.output:
                 yield p, step.output[0]
 
-    prev = None
     queued = {}
+    if pipelined:
+        # the drain thread needs the GIL around its engine call; at the default 5 ms switch
+        # interval it would wait that long for the flows to yield, twice per drain
+        old_switch = sys.getswitchinterval()
+        sys.setswitchinterval(2e-4)
+    try:
+        yield from _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, queued)
+    finally:
+        if pipelined:
+            sys.setswitchinterval(old_switch)
+
+
+def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, queued):
+    prev = None
     for w0 in range(0, len(msgs), window):
         batch = msgs[w0:w0 + window]
         for p, j in batch:
