@@ -221,8 +221,7 @@ HP_D H6 h6_neg(const H6& a) { return {fp_neg(a.c0), fp_neg(a.c1), fp_neg(a.c2)};
 HP_D H6 h6_red(const H6& a) { return {fp_reduce(a.c0), fp_reduce(a.c1), fp_reduce(a.c2)}; }
 HP_D H6 h6_mul_v(const H6& a) { return {h_mul_xi(a.c2), a.c0, a.c1}; }
 
-// Karatsuba (stower.hpp f6_mul), inputs < 4p; outputs reduced (each one sum formed unnormalised
-// and reduced in one pass)
+// Karatsuba (stower.hpp f6_mul), inputs < 4p
 HP_D H6 h6_mul(const H6& a, const H6& b) {
   const Fp v0 = h_mul(a.c0, b.c0);
   const Fp v1 = h_mul(a.c1, b.c1);
@@ -230,8 +229,8 @@ HP_D H6 h6_mul(const H6& a, const H6& b) {
   const Fp t0 = h_mul(fp_addl(a.c1, a.c2), fp_add(b.c1, b.c2));
   const Fp t1 = h_mul(fp_addl(a.c0, a.c1), fp_add(b.c0, b.c1));
   const Fp t2 = h_mul(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2));
-  return {fp_red_l(h_add_xi_l(v0, fp_sub2l(t0, v1, v2))), fp_red_l(h_add_xi_l(fp_sub2l(t1, v0, v1), v2)),
-          fp_red_l(fp_addl(fp_sub2l(t2, v0, v2), v1))};
+  return {fp_add(v0, h_mul_xi(fp_sub(fp_subl(t0, v1), v2))), fp_add(fp_sub(fp_subl(t1, v0), v1), h_mul_xi(v2)),
+          fp_add(fp_sub(fp_subl(t2, v0), v2), v1)};
 }
 // x (a + b v)
 HP_D H6 h6_mul_01(const H6& x, const Fp& a, const Fp& b) {
@@ -274,16 +273,13 @@ HP_D H12 h12_mul(const H12& a, const H12& b) {
   const H6 t0 = h6_mul(a.c0, b.c0);
   const H6 t1 = h6_mul(a.c1, b.c1);
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_add(b.c0, b.c1));
-  return h12_kcomb(t0, t1, s);
+  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
 }
 // complex squaring (stower.hpp f12_sqr)
 HP_D H12 h12_sqr(const H12& a) {
-  const H6 t = h6_mul(a.c0, a.c1);
+  const H6 t = h6_red(h6_mul(a.c0, a.c1));
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_red(h6_add(a.c0, h6_mul_v(a.c1))));
-  // (s - t - v t, 2 t)
-  return {{fp_red_l(fp_sub2l(s.c0, t.c0, h_xi_l(t.c2))), fp_red_l(fp_sub2l(s.c1, t.c1, t.c0)),
-           fp_red_l(fp_sub2l(s.c2, t.c2, t.c1))},
-          {fp_red_mk<2, 0>(t.c0, t.c0), fp_red_mk<2, 0>(t.c1, t.c1), fp_red_mk<2, 0>(t.c2, t.c2)}};
+  return h12_red({h6_sub(h6_sub(s, t), h6_mul_v(t)), h6_add(t, t)});
 }
 // f (c0 + c1 w^2 + c4 w^3); c0, c1, c4 normalised, < 2p
 HP_D H12 h12_mul_014(const H12& f, const Fp& c0, const Fp& c1, const Fp& c4) {
@@ -292,7 +288,7 @@ HP_D H12 h12_mul_014(const H12& f, const Fp& c0, const Fp& c1, const Fp& c4) {
   const H6 t0 = h6_red(h6_mul_01(f.c0, c0, c1));
   const H6 t1 = h6_red(h6_mul_1(f.c1, c4));
   const H6 s = h6_red(h6_mul_01(fs, c0, c14));
-  return h12_kcomb(t0, t1, s);
+  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
 }
 // x (b1 v + b2 v^2): c0 = xi (a1 b2 + a2 b1), c1 = a0 b1 + xi a2 b2, c2 = a0 b2 + a1 b1 (5 products)
 HP_D H6 h6_mul_12(const H6& x, const Fp& b1, const Fp& b2) {
@@ -316,13 +312,13 @@ HP_D H12 h12_mul_lines(const H12& f, const Fp& a0, const Fp& a1, const Fp& a4, c
   const Fp y2 = fp_sub(fp_subl(h_mul(fp_addl(a1, a4), fp_add(b1, b4)), a1b1), a4b4);
   const H6 C0 = h6_red({fp_add(a0b0, h_mul_xi(a4b4)), x1, a1b1});
   const Fp c11 = fp_reduce(y1), c12 = fp_reduce(y2);
-  const H6 t0 = h6_mul(f.c0, C0);
+  const H6 t0 = h6_red(h6_mul(f.c0, C0));
   const H6 t1 = h6_red(h6_mul_12(f.c1, c11, c12));
-  const H6 s = h6_mul(h6_add(f.c0, f.c1), h6_red({C0.c0, fp_add(C0.c1, c11), fp_add(C0.c2, c12)}));
-  return h12_kcomb(t0, t1, s);
+  const H6 s = h6_red(h6_mul(h6_add(f.c0, f.c1), h6_red({C0.c0, fp_add(C0.c1, c11), fp_add(C0.c2, c12)})));
+  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
 }
 HP_D H12 h12_inv(const H12& a) {
-  const H6 t = h6_red(h6_sub(h6_mul(a.c0, a.c0), h6_red(h6_mul_v(h6_mul(a.c1, a.c1)))));
+  const H6 t = h6_red(h6_sub(h6_red(h6_mul(a.c0, a.c0)), h6_red(h6_mul_v(h6_red(h6_mul(a.c1, a.c1))))));
   const H6 ti = h6_red(h6_inv(t));
   return h12_red({h6_mul(a.c0, ti), h6_neg(h6_mul(a.c1, ti))});
 }
@@ -369,7 +365,7 @@ HP_D H12 h12_cyclo_sqr(const H12& f) {
   {
     const Fp s2 = h_sqr(a2), s5 = h_sqr(a5), s25 = h_sqr(fp_add(a2, a5));
     r.c0.c2 = fp_red_mk<3, -2>(h_add_xi_l(s2, s5), a4);
-    r.c1.c0 = fp_red_mk<3, 2>(h_xi_l(fp_sub2l(s25, s2, s5)), a1);
+    r.c1.c0 = fp_red_mk<3, 2>(h_add_xi_l(fp_zero(), fp_sub2l(s25, s2, s5)), a1);
   }
   return r;
 }
