@@ -21,6 +21,17 @@ def _u32(idx, n):
     return a, a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _check_bivar(t, commits, part_idx):
+    """Every BivarCommitment of a degree-t call holds (t+1)(t+2)/2 points, and every request names
+    one of them: the kernels stride through the joined buffer by that count."""
+    ncoef = (t + 1) * (t + 2) // 2
+    for k, c in enumerate(commits):
+        if len(c) != ncoef:
+            raise ValueError("commitment %d has %d points, degree %d needs %d" % (k, len(c), t, ncoef))
+    if any(not 0 <= int(i) < len(commits) for i in part_idx):
+        raise ValueError("commitment index out of range")
+
+
 def _join(points, size):
     if isinstance(points, (bytes, bytearray)):
         b = bytes(points)
@@ -204,6 +215,7 @@ class Engine:
 
     def bivar_row(self, t, commits, part_idx, xs):
         """BivarCommitment::row(x) (src/sync_key_gen.rs:496) for each (part, x)."""
+        _check_bivar(t, commits, part_idx)
         cb = _join([c for part in commits for c in part], G1_BYTES)
         nrow = len(part_idx)
         pa, ppa = _u32(part_idx, nrow)
@@ -251,6 +263,7 @@ class Engine:
 
     def bivar_ack_check(self, t, commits, part_idx, xs, ys, vals):
         """BivarCommitment::evaluate(x, y) == g1 * val (src/sync_key_gen.rs:542) per ack."""
+        _check_bivar(t, commits, part_idx)
         cb = _join([c for part in commits for c in part], G1_BYTES)
         n = len(part_idx)
         pa, ppa = _u32(part_idx, n)

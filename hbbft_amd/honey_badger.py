@@ -30,8 +30,8 @@ import sys
 import time
 
 from . import hoststage
-from .protocol import BatchVerifier, Ciphertext, Deferred, NetworkInfo, ThresholdDecrypt, ThresholdSign, \
-    signature_parity
+from .protocol import BatchVerifier, Ciphertext, Deferred, NetworkInfo, ProtocolError, Step, ThresholdDecrypt, \
+    ThresholdSign, signature_parity
 from .sync_key_gen import G1_GEN, R_ORDER
 
 __all__ = ["NetworkKeys", "EpochTrace", "coin_document", "run_epoch", "EpochResult"]
@@ -131,6 +131,7 @@ class EpochResult:
         self.signatures = {}   # proposer -> combined signature (ABI G2)
         self.plaintexts = {}   # proposer -> bytes
         self.faults = []       # (instance kind, proposer, Fault)
+        self.errors = []       # (instance kind, proposer, ProtocolError): the reference's Err results
         self.timing = {}       # phase -> seconds
         self.engine_calls = 0
         self.checks_gpu = 0    # checks drained through the engine (incl. post-termination window tail)
@@ -152,22 +153,16 @@ def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelin
     -- same verdicts, fewer checks drained for instances that terminate early."""
     def hand(batch):
         for p, j in batch:
-            step = handle(p, j)
+            try:
+                step = handle(p, j)
+            except ProtocolError as e:  # the reference's Err from handle_message (immediate combines)
+                res.errors.append((kind, p, e))
+                continue
             res.faults += [(kind, p, f) for f in step.fault_log]
             if step.output:
                 yield p, step.output[0]
 
-    queued = {}
-    if pipelined:
-        # the drain thread needs the GIL around its engine call; at the default 5 ms switch
-        # interval it would wait that long for the flows to yield, twice per drain
-        old_switch = sys.getswitchinterval()
-        sys.setswitchinterval(2e-4)
-    try:
-        yield from _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, queued)
-    finally:
-        if pipelined:
-            sys.setswitchinterval(old_switch)
+    yield from _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, {})
 
 
 def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, queued):
@@ -193,14 +188,30 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
         yield from hand(prev)
 
 
-def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True, slack=4):
+def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True, slack=4, switch_interval=2e-4,
+              defer=True):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
-    ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share)."""
+    ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
+    ``switch_interval``: the interpreter's thread switch interval while the epoch runs pipelined
+    (the drain thread needs the GIL around its engine call; at the default 5 ms it waits that long
+    for the flows to yield, twice per drain); restored on return.  None leaves it alone.
+    ``defer``: combines run in one batch at the end of the epoch (False: one engine call each,
+    when the instance asks; the reference's order, used to check the deferred path)."""
+    old = sys.getswitchinterval()
+    if pipelined and switch_interval:
+        sys.setswitchinterval(switch_interval)
+    try:
+        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer)
+    finally:
+        sys.setswitchinterval(old)
+
+
+def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     ver = BatchVerifier(engine)
-    ver.recording = True                   # combines of the epoch run in one batch at the end
+    ver.recording = defer                  # combines of the epoch run in one batch at the end
     sk = keys.sks[our]
     n = keys.n
     t_all = time.perf_counter()
@@ -222,13 +233,19 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True
     t0 = time.perf_counter()
     coin_out = {}
     for p, inst in ts.items():
-        step = inst.handle_input()
+        step = _input(inst, "coin", p, res)
+        res.faults += [("coin", p, f) for f in step.fault_log]
         if step.output:
             coin_out[p] = step.output[0]
+    handed = {}  # (kind, proposer) -> senders handed to the instance, in order (for a replay)
+
+    def hand_coin(p, j):
+        handed.setdefault(("coin", p), []).append(j)
+        return ts[p].handle_message(j, trace.coin_shares[(p, j)])
+
     for p, out in _deliver(ver, trace.coin_msgs, window, ts,
                            lambda p, j: ver.queue_sig(keys.pks[j], ts[p].doc_hash, trace.coin_shares[(p, j)]),
-                           lambda p, j: ts[p].handle_message(j, trace.coin_shares[(p, j)]), res, "coin", pipelined,
-                           limit):
+                           hand_coin, res, "coin", pipelined, limit):
         coin_out[p] = out
     res.timing["coin_verify"] = time.perf_counter() - t0
 
@@ -249,37 +266,90 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True
     dec_out = {}
     for p in ps:
         td[p].set_ciphertext(cts[p])
-        step = td[p].handle_input()
+        step = _input(td[p], "dec", p, res)
         res.faults += [("dec", p, f) for f in step.fault_log]
         if step.output:
             dec_out[p] = step.output[0]
+
+    def hand_dec(p, j):
+        handed.setdefault(("dec", p), []).append(j)
+        return td[p].handle_message(j, trace.dec_shares[(p, j)])
+
     for p, out in _deliver(ver, trace.dec_msgs, window, td,
                            lambda p, j: ver.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], cts[p].huv, cts[p].w),
-                           lambda p, j: td[p].handle_message(j, trace.dec_shares[(p, j)]), res, "dec", pipelined,
-                           limit):
+                           hand_dec, res, "dec", pipelined, limit):
         dec_out[p] = out
     res.timing["decrypt_verify"] = time.perf_counter() - t0
 
     # --- deferred combines: one G2 combine+verify batch, one G1 interpolation batch
     t0 = time.perf_counter()
-    ver.flush_combines()
+    failed = {id(d) for d in ver.flush_combines()}
     res.timing["combine"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    sigs = {}
-    for p, d in coin_out.items():
-        sig, st, ok = d.result if isinstance(d, Deferred) else (d, 0, True)
-        if st != 0 or not ok:
-            raise RuntimeError("coin %d: combined signature does not verify" % p)
-        sigs[p] = sig
+    # A failed deferred combine: the reference returned Err from the call that triggered it (and a
+    # ThresholdSign stayed open), so that instance is replayed with immediate combines; its Steps
+    # (outputs, faults, errors) replace the optimistic ones.
+    for kind, outs in (("coin", coin_out), ("dec", dec_out)):
+        for p in [p for p, d in outs.items() if isinstance(d, Deferred) and id(d) in failed]:
+            del outs[p]
+            res.faults = [f for f in res.faults if f[:2] != (kind, p)]
+            out = _replay(engine, kind, p, ni_sign if kind == "coin" else ni_dec,
+                          ts[p].doc_hash if kind == "coin" else cts[p], handed.get((kind, p), []),
+                          trace.coin_shares if kind == "coin" else trace.dec_shares, res)
+            if out is not None:
+                outs[p] = out
+    sigs = {p: (d.result[0] if isinstance(d, Deferred) else d) for p, d in coin_out.items()}
     order = sorted(sigs)
     res.signatures = sigs
     res.coins = dict(zip(order, hoststage.signature_parity([sigs[p] for p in order]))) if order else {}
     order = sorted(dec_out)
+    direct = {p: dec_out[p] for p in order if not isinstance(dec_out[p], Deferred)}
+    order = [p for p in order if p not in direct]
     gs = [dec_out[p].result[0] for p in order]
     res.plaintexts = dict(zip(order, hoststage.xor_with_hash(gs, [dec_out[p].data for p in order],
                                                               threads=threads))) if order else {}
+    res.plaintexts.update(direct)
     res.timing["output"] = time.perf_counter() - t0
     res.timing["epoch"] = time.perf_counter() - t_all
     res.engine_calls, res.checks_gpu, res.checks_consumed = ver.calls, ver.checks, ver.lookups
     res.combines = len(coin_out) + len(dec_out)
     return res
+
+
+def _input(inst, kind, p, res):
+    """inst.handle_input(); the reference's Err is recorded (an empty Step is returned)."""
+    try:
+        return inst.handle_input()
+    except ProtocolError as e:
+        res.errors.append((kind, p, e))
+        return Step()
+
+
+def _replay(engine, kind, p, netinfo, doc_or_ct, senders, shares, res):
+    """Re-run one instance with immediate combines (a fresh, non-recording verifier): its input,
+    then every message it was handed, in order.  An Err of the reference is recorded in
+    ``res.errors`` and handling continues, as a caller of the reference's handle_message would.
+    Returns the instance's output (signature / plaintext) or None."""
+    ver = BatchVerifier(engine)
+    inst = ThresholdSign(netinfo, ver) if kind == "coin" else ThresholdDecrypt(netinfo, ver)
+    output = None
+
+    def run(call):
+        nonlocal output
+        try:
+            step = call()
+        except ProtocolError as e:
+            res.errors.append((kind, p, e))
+            return
+        res.faults += [(kind, p, f) for f in step.fault_log]
+        if step.output and output is None:
+            output = step.output[0]
+
+    if kind == "coin":
+        inst.set_document_hash(doc_or_ct)
+    else:
+        inst.set_ciphertext(doc_or_ct)
+    run(inst.handle_input)
+    for j in senders:
+        run(lambda: inst.handle_message(j, shares[(p, j)]))
+    return output

@@ -107,11 +107,22 @@ class NetworkInfo:
 class Deferred:
     """A combine recorded by a BatchVerifier in deferred mode; ``flush_combines`` fills ``result``
     ((signature, status, verdict) for G2, (point, status) for G1).  ``data`` carries the
-    ciphertext's V for a deferred decryption (the plaintext is xor_with_hash(result[0], data))."""
+    ciphertext's V for a deferred decryption (the plaintext is xor_with_hash(result[0], data)).
+
+    ``ok`` says whether the combine succeeded.  A deferred combine lets its instance terminate
+    optimistically; when it failed, the reference would have returned ``Err`` from the call that
+    triggered it and (ThresholdSign) stayed open, so the driver replays that instance's inputs with
+    immediate combines (honey_badger.run_epoch) -- the Steps and errors are then the reference's."""
     __slots__ = ("key", "result", "data")
 
     def __init__(self, key, data=None):
         self.key, self.result, self.data = key, None, data
+
+    @property
+    def ok(self):
+        if self.result is None:
+            raise RuntimeError("deferred combine not flushed")
+        return self.result[1] == 0 and (len(self.result) == 2 or self.result[2])
 
 
 class BatchVerifier:
@@ -126,13 +137,12 @@ class BatchVerifier:
         self.calls = 0
         self.checks = 0
         self.max_batch = 0
-        # combines: results by input, and (when recording) the requests a dry run made
-        self._comb_g2, self._comb_g1 = {}, {}
         self.recording = False  # deferred mode: combines return Deferred, run later in one batch
         self.lookups = 0        # verdicts the flows consumed (the checks the reference performs)
         self._docs = {}
         self._rec_g2, self._rec_g1 = [], []
         self._released = set()  # instances released since the last drain was stored
+        self._open = {}         # instance key -> number of running instances that use it
         self._inflight = 0      # drain_async calls not yet committed
 
     # -------------------------------------------------------------- host hashing
@@ -153,8 +163,6 @@ class BatchVerifier:
         verdict) from the cache, or one engine call.  While recording, the request is noted and a
         valid placeholder is returned (the state machine does not depend on the signature)."""
         key = (t, tuple(idx), tuple(bytes(s) for s in shares), bytes(master_pk), bytes(h))
-        if key in self._comb_g2:
-            return self._comb_g2.pop(key)  # one combine per instance: consumed on use
         if self.recording:
             d = Deferred(key)
             self._rec_g2.append(d)
@@ -166,8 +174,6 @@ class BatchVerifier:
     def interpolate_g1(self, t, idx, shares):
         """PublicKeySet::decrypt's interpolation (src/threshold_decrypt.rs:242-250): (point, status)."""
         key = (t, tuple(idx), tuple(bytes(s) for s in shares))
-        if key in self._comb_g1:
-            return self._comb_g1.pop(key)
         if self.recording:
             d = Deferred(key)
             self._rec_g1.append(d)
@@ -178,7 +184,7 @@ class BatchVerifier:
 
     def flush_combines(self):
         """Run every deferred combine: one engine call per (t, master key) for G2 and per t for G1;
-        fills each Deferred's result."""
+        fills each Deferred's result; returns the Deferreds whose combine failed."""
         groups = {}
         for d in self._rec_g2:
             groups.setdefault((d.key[0], d.key[3]), []).append(d)
@@ -196,24 +202,51 @@ class BatchVerifier:
             self.calls += 1
             for d, o, s_ in zip(ds, out, st):
                 d.result = (o, s_)
+        failed = [d for d in self._rec_g2 + self._rec_g1 if not d.ok]
         self._rec_g2, self._rec_g1 = [], []
+        return failed
+
+    # Instances are reference-counted by their key (document hash; (H_uv, W) for a ciphertext):
+    # two running instances may share one (a Byzantine proposer can copy another's ciphertext, two
+    # BA instances could sign the same document), and a release drops the cached verdicts only
+    # when the last of them terminates.
+    def open_doc(self, h):
+        self._open_key(bytes(h))
+
+    def open_ct(self, huv, w):
+        self._open_key((bytes(huv), bytes(w)))
+
+    def _open_key(self, key):
+        self._open[key] = self._open.get(key, 0) + 1
+        self._released.discard(key)
+
+    def _close_key(self, key):
+        """True when the last running instance of ``key`` is gone."""
+        n = self._open.get(key, 0) - 1
+        if n > 0:
+            self._open[key] = n
+            return False
+        self._open.pop(key, None)
+        self._released.add(key)
+        return True
 
     def release_doc(self, h):
-        """Drop the cached verdicts of a terminated ThresholdSign instance (document hash h)."""
-        self._sig.pop(bytes(h), None)
-        self._released.add(bytes(h))
+        """A ThresholdSign instance (document hash h) terminated: drop the cached verdicts if no
+        other running instance signs the same document."""
+        if self._close_key(bytes(h)):
+            self._sig.pop(bytes(h), None)
 
     def release_ct(self, huv, w):
-        """Drop the cached verdicts of a terminated ThresholdDecrypt instance."""
+        """A ThresholdDecrypt instance terminated (or its ciphertext was rejected): drop the cached
+        verdicts if no other running instance holds the same ciphertext."""
         key = (bytes(huv), bytes(w))
-        self._dec.pop(key, None)
-        self._ct.pop(key, None)
-        self._released.add(key)
+        if self._close_key(key):
+            self._dec.pop(key, None)
+            self._ct.pop(key, None)
 
     def cached(self):
         return (sum(len(d) for d in self._sig.values()) + sum(len(d) for d in self._dec.values())
-                + sum(len(d) for d in self._ct.values())
-                + len(self._comb_g1) + len(self._comb_g2))
+                + sum(len(d) for d in self._ct.values()))
 
     # Verdicts are kept per instance (document hash / ciphertext) so that a terminated instance's
     # entries are released in O(1).
@@ -226,10 +259,11 @@ class BatchVerifier:
     def sig_valid(self, pk, h, share):
         self.lookups += 1
         h, k = bytes(h), (bytes(pk), bytes(share))
-        if k not in self._sig.get(h, ()):
+        v = self._sig.get(h, {}).get(k)
+        if v is None:
             self._qsig.append((k[0], h, k[1]))
-            self.drain()
-        return self._sig[h][k]
+            v = self.drain()[("sig", h, k)]
+        return v
 
     # ThresholdDecrypt: PublicKeyShare::verify_decryption_share(share, ct)  (src/threshold_decrypt.rs:227)
     def queue_dec(self, pk, share, huv, w):
@@ -240,10 +274,11 @@ class BatchVerifier:
     def dec_valid(self, pk, share, huv, w):
         self.lookups += 1
         c, k = (bytes(huv), bytes(w)), (bytes(pk), bytes(share))
-        if k not in self._dec.get(c, ()):
+        v = self._dec.get(c, {}).get(k)
+        if v is None:
             self._qdec.append(k + c)
-            self.drain()
-        return self._dec[c][k]
+            v = self.drain()[("dec", c, k)]
+        return v
 
     # Ciphertext::verify  (src/threshold_decrypt.rs:142)
     def queue_ct(self, ct):
@@ -254,14 +289,17 @@ class BatchVerifier:
     def ct_valid(self, ct):
         self.lookups += 1
         c, u = (bytes(ct.huv), bytes(ct.w)), bytes(ct.u)
-        if u not in self._ct.get(c, ()):
+        v = self._ct.get(c, {}).get(u)
+        if v is None:
             self._qct.append((u, c[1], c[0]))
-            self.drain()
-        return self._ct[c][u]
+            v = self.drain()[("ct", c, u)]
+        return v
 
     def drain(self):
-        """Verify everything queued: one engine call per kind."""
-        self._store(self._run_jobs(self._take_jobs()))
+        """Verify everything queued: one engine call per kind.  Returns the fresh verdicts by
+        (kind, instance key, item key) -- a synchronous *_valid reads its verdict from there even
+        when no running instance keeps it cached."""
+        return self._store(self._run_jobs(self._take_jobs()))
 
     def drain_async(self):
         """Start verifying everything queued on a worker thread (one engine call per kind, the
@@ -281,7 +319,7 @@ class BatchVerifier:
             res = pending.result()
         finally:
             self._inflight -= 1
-        self._store(res)
+        return self._store(res)
 
     def _take_jobs(self):
         """Snapshot the queues as engine-call arguments (main thread)."""
@@ -311,26 +349,35 @@ class BatchVerifier:
         return [(kind, keys, fn[kind](*args)) for kind, keys, args in jobs]
 
     def _store(self, results):
-        """Cache verdicts (main thread).  Verdicts of instances released while their drain was in
-        flight are dropped, so a terminated instance leaves nothing behind."""
+        """Cache verdicts (main thread) and return them as {(kind, instance, item): verdict}.
+        Verdicts of instances whose last running instance terminated while the drain was in
+        flight are not cached, so a terminated instance leaves nothing behind."""
+        fresh = {}
+        rel = self._released
         for kind, keys, v in results:
             self._count(len(keys))
             if kind == "ct":
                 for k, ok in zip(keys, v):
-                    if (k[2], k[1]) not in self._released:
-                        self._ct.setdefault((k[2], k[1]), {})[k[0]] = bool(ok)
+                    c = (k[2], k[1])
+                    fresh[("ct", c, k[0])] = bool(ok)
+                    if c not in rel:
+                        self._ct.setdefault(c, {})[k[0]] = bool(ok)
             elif kind == "sig":
                 for k, ok in zip(keys, v):
-                    if k[1] not in self._released:
+                    fresh[("sig", k[1], (k[0], k[2]))] = bool(ok)
+                    if k[1] not in rel:
                         self._sig.setdefault(k[1], {})[(k[0], k[2])] = bool(ok)
             else:
                 for k, ok in zip(keys, v):
-                    if (k[2], k[3]) not in self._released:
-                        self._dec.setdefault((k[2], k[3]), {})[(k[0], k[1])] = bool(ok)
-        # nothing queued after a release can name the released instance (the drivers queue only
-        # for running instances), so the set only has to outlive the drains in flight at release
+                    c = (k[2], k[3])
+                    fresh[("dec", c, (k[0], k[1]))] = bool(ok)
+                    if c not in rel:
+                        self._dec.setdefault(c, {})[(k[0], k[1])] = bool(ok)
+        # nothing queued after the last release can name the released instance (the drivers
+        # queue only for running instances), so the set only has to outlive the drains in flight
         if not self._inflight:
             self._released.clear()
+        return fresh
 
     def _count(self, n):
         self.calls += 1
@@ -356,6 +403,7 @@ class ThresholdSign:
         if self.doc_hash is not None:
             raise ProtocolError("MultipleMessagesToSign")
         self.doc_hash = self.verifier.hash_doc(doc)
+        self.verifier.open_doc(self.doc_hash)
 
     def set_document_hash(self, h):
         """``set_document`` with H already computed, e.g. by a driver that hashes the documents of
@@ -363,6 +411,7 @@ class ThresholdSign:
         if self.doc_hash is not None:
             raise ProtocolError("MultipleMessagesToSign")
         self.doc_hash = bytes(h)
+        self.verifier.open_doc(self.doc_hash)
 
     def handle_input(self):
         return self.sign()
@@ -472,7 +521,9 @@ class ThresholdDecrypt:
     def set_ciphertext(self, ct):  # :138-147
         if self.ciphertext is not None:
             raise ProtocolError("MultipleInputs")
+        self.verifier.open_ct(ct.huv, ct.w)
         if not self.verifier.ct_valid(ct):
+            self.verifier.release_ct(ct.huv, ct.w)
             raise ProtocolError("InvalidCiphertext")
         self.ciphertext = ct
 

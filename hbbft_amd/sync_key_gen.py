@@ -59,15 +59,25 @@ def interpolate_at_zero(samples):
     return acc
 
 
+def ncoef(degree):
+    """Points of a degree-d BivarCommitment: (d+1)(d+2)/2 (coeff_pos(d, d) + 1)."""
+    return (degree + 1) * (degree + 2) // 2
+
+
 def ser_row(coeffs):
     return len(coeffs).to_bytes(8, "little") + b"".join(c.to_bytes(32, "little") for c in coeffs)
 
 
-def de_row(b, expect_len):
+def de_row(b):
+    """bincode::deserialize::<Poly> (sync_key_gen.rs:507): a u64 LE coefficient count, then that many
+    32-byte LE canonical Fr.  bincode 1.x's ``deserialize`` reads what the type needs and ignores
+    trailing bytes; a short buffer or a non-canonical Fr is an error (None).  Any count
+    deserialises: a row of the wrong length is caught by the commitment comparison (RowCommitment),
+    as in the reference."""
     if len(b) < 8:
         return None
     n = int.from_bytes(b[:8], "little")
-    if n != expect_len or len(b) != 8 + 32 * n:
+    if len(b) < 8 + 32 * n:
         return None
     out = [int.from_bytes(b[8 + 32 * k:40 + 32 * k], "little") for k in range(n)]
     return out if all(c < R_ORDER for c in out) else None
@@ -78,9 +88,11 @@ def ser_val(v):
 
 
 def de_val(b):
-    if len(b) != 32:
+    """bincode::deserialize::<FieldWrap<Fr>> (sync_key_gen.rs:539-541): 32 bytes LE, canonical;
+    trailing bytes are ignored (bincode 1.x), fewer than 32 bytes or a value >= r is an error."""
+    if len(b) < 32:
         return None
-    v = int.from_bytes(b, "little")
+    v = int.from_bytes(b[:32], "little")
     return v if v < R_ORDER else None
 
 
@@ -97,10 +109,17 @@ class Ciphertext:
 
 
 class Part:
-    """Part(BivarCommitment, Vec<Ciphertext>) (sync_key_gen.rs:225)."""
+    """Part(BivarCommitment, Vec<Ciphertext>) (sync_key_gen.rs:225).
+
+    A BivarCommitment of degree d holds exactly ncoef(d) points (threshold_crypto builds it that
+    way; a message that carries another count does not decode, see wire.decode_part), so a Part
+    with an inconsistent count cannot be constructed: the batched engine calls rely on it."""
 
     def __init__(self, degree, commit, rows):
-        self.degree, self.commit, self.rows = degree, [bytes(c) for c in commit], list(rows)
+        self.degree, self.commit, self.rows = int(degree), [bytes(c) for c in commit], list(rows)
+        if self.degree < 0 or len(self.commit) != ncoef(self.degree):
+            raise ValueError("BivarCommitment of degree %d needs %d points, got %d"
+                             % (self.degree, ncoef(max(self.degree, 0)), len(self.commit)))
 
     def __eq__(self, o):
         return isinstance(o, Part) and (self.degree, self.commit, self.rows) == (o.degree, o.commit, o.rows)
@@ -141,8 +160,12 @@ class ProposalState:
         self.values = {}   # sender index + 1 -> Fr
         self.acks = set()  # sender indices
 
-    def same_commit(self, part):
-        return part.degree == self.degree and part.commit == self.commit
+    def equals_new(self, part):
+        """``*state == ProposalState::new(commit)`` (sync_key_gen.rs:489): the derived PartialEq
+        compares the commitment AND the recorded values and acks, so once any Ack was handled for
+        this proposer even an identical Part is ``MultipleParts``."""
+        return (part.degree == self.degree and part.commit == self.commit
+                and not self.values and not self.acks)
 
     def is_complete(self, threshold):
         return len(self.acks) > 2 * threshold
@@ -254,7 +277,6 @@ class SyncKeyGen:
     def handle_parts(self, items, rng=None):
         rng = rng or random.SystemRandom()
         n = len(self.pub_keys)
-        t = self.threshold
         # 1. sequential state pass: which parts are new, what each outcome depends on
         plan = []
         seen = {}
@@ -267,32 +289,42 @@ class SyncKeyGen:
                 continue
             state = self.parts.get(sidx) or seen.get(sidx)
             if state is not None:
-                plan.append(("fault", "MultipleParts") if not state.same_commit(part) else ("none", None))
+                plan.append(("fault", "MultipleParts") if not state.equals_new(part) else ("none", None))
                 continue
             st = ProposalState(part.degree, part.commit)
             seen[sidx] = st
             plan.append(("new", (sidx, part, st)))
         new = [p[1] for p in plan if p[0] == "new"]
-        # 2. crypto in batches: our commitment rows, our decrypted rows, the rows' commitments
+        # 2. crypto in batches: our commitment rows, our decrypted rows, the rows' commitments.
+        #    Parts may carry any degree (the reference accepts them); one engine call per degree.
         rows_ok = {}
         if new and self.our_idx is not None:
             x = self.our_idx + 1
-            commit_rows = self.engine.bivar_row(t, [p.commit for _, p, _ in new], list(range(len(new))),
-                                                [x] * len(new))
+            commit_rows = [None] * len(new)
+            for d, js in _by_degree(range(len(new)), lambda j: new[j][1].degree).items():
+                got = self.engine.bivar_row(d, [new[j][1].commit for j in js], list(range(len(js))), [x] * len(js))
+                for j, r in zip(js, got):
+                    commit_rows[j] = r
             plain = _decrypt_batch(self.engine, self.sec_key, [p.rows[self.our_idx] for _, p, _ in new], self.threads)
-            polys = [de_row(b, t + 1) if b is not None else None for b in plain]
-            flat = [c for poly in polys if poly is not None for c in poly]
+            polys = [de_row(b) if b is not None else None for b in plain]
+            # Poly::commitment() only where the lengths agree: a row of another length can never
+            # equal the commitment row (Commitment's derived PartialEq compares the vectors)
+            match = [j for j in range(len(new)) if polys[j] is not None and len(polys[j]) == len(commit_rows[j])]
+            flat = [c for j in match for c in polys[j]]
             comm = self.engine.g1_mul_gen(flat) if flat else []
-            k = 0
+            row_comm, k = {}, 0
+            for j in match:
+                row_comm[j] = comm[k:k + len(polys[j])]
+                k += len(polys[j])
             for j, (sidx, part, st) in enumerate(new):
                 if plain[j] is None:
                     rows_ok[sidx] = ("fault", "DecryptRow")
                 elif polys[j] is None:
                     rows_ok[sidx] = ("fault", "DeserializeRow")
+                elif row_comm.get(j) == commit_rows[j]:
+                    rows_ok[sidx] = ("row", polys[j])
                 else:
-                    got = comm[k:k + t + 1]
-                    k += t + 1
-                    rows_ok[sidx] = ("row", polys[j]) if got == commit_rows[j] else ("fault", "RowCommitment")
+                    rows_ok[sidx] = ("fault", "RowCommitment")
         # 3. apply in order; encrypt the Acks of valid rows in one host batch
         outs, ack_jobs = [], []
         for kind, val in plan:
@@ -351,18 +383,19 @@ class SyncKeyGen:
             plain = _decrypt_batch(self.engine, self.sec_key, [a.values[self.our_idx] for _, a, _ in new], self.threads)
             vals = [de_val(b) if b is not None else None for b in plain]
             chk = [j for j, v in enumerate(vals) if v is not None]
-            ok = b""
-            if chk:
+            okmap = {}
+            # one hbh_bivar_ack_check per commitment degree; each part's commitment joined once
+            for d, js in _by_degree(chk, lambda j: new[j][2].degree).items():
                 commits, cidx = [], {}
-                for j in chk:
+                for j in js:
                     p = new[j][1].proposer_idx
                     if p not in cidx:
                         cidx[p] = len(commits)
                         commits.append(new[j][2].commit)
-                ok = self.engine.bivar_ack_check(self.threshold, commits, [cidx[new[j][1].proposer_idx] for j in chk],
-                                                 [self.our_idx + 1] * len(chk), [new[j][0] + 1 for j in chk],
-                                                 [vals[j] for j in chk])
-            okmap = dict(zip(chk, ok))
+                ok = self.engine.bivar_ack_check(d, commits, [cidx[new[j][1].proposer_idx] for j in js],
+                                                 [self.our_idx + 1] * len(js), [new[j][0] + 1 for j in js],
+                                                 [vals[j] for j in js])
+                okmap.update(zip(js, ok))
             for j in range(len(new)):
                 if plain[j] is None:
                     verdict[j] = ("fault", "DecryptValue")
@@ -395,19 +428,33 @@ class SyncKeyGen:
 
     # -------------------------------------------------------------- generate (sync_key_gen.rs:444-462)
     def generate(self):
-        """(PublicKeySet, secret key share or None): sum of row(0) of the complete parts' commitments;
+        """(PublicKeySet, secret key share or None) (sync_key_gen.rs:444-462): pk_commit starts as
+        Poly::zero().commitment() (empty) and ``+= part.commit.row(0)`` for every complete part --
+        Commitment's AddAssign resizes to the longer operand and removes trailing zero points --;
         our share = sum over those parts of the interpolation at 0 of the first t+1 values."""
         t = self.threshold
         complete = [self.parts[k] for k in sorted(self.parts) if self.parts[k].is_complete(t)]
-        commit = [bytes(G1_BYTES)] * (t + 1)
+        zero = bytes(G1_BYTES)
+        commit = []
         sk = 0 if self.our_idx is not None else None
         for part in complete:
-            row0 = [part.commit[coeff_pos(i, 0)] for i in range(t + 1)]  # row(0)_i = C(i, 0)
-            commit = hoststage.g1_add(commit, row0)
+            row0 = [part.commit[coeff_pos(i, 0)] for i in range(part.degree + 1)]  # row(0)_i = C(i, 0)
+            m = max(len(commit), len(row0))
+            commit = hoststage.g1_add(commit + [zero] * (m - len(commit)), row0 + [zero] * (m - len(row0)))
+            while commit and commit[-1] == zero:
+                commit.pop()
             if sk is not None:
                 samples = sorted(part.values.items())[: t + 1]
                 sk = (sk + interpolate_at_zero(samples)) % R_ORDER
         return PublicKeySet(commit), sk
+
+
+def _by_degree(items, degree):
+    """Group items by commitment degree (order kept within a group)."""
+    groups = {}
+    for it in items:
+        groups.setdefault(degree(it), []).append(it)
+    return groups
 
 
 __all__ = ["SyncKeyGen", "Part", "Ack", "PartOutcome", "AckOutcome", "PublicKeySet", "Ciphertext",

@@ -72,3 +72,61 @@ def test_duplicates_are_checked_once():
     _fill(ver, docs=1)                   # already cached: nothing queued
     ver.drain()
     assert [c[:2] for c in eng.calls] == [("sig", 5)]
+
+
+def test_shared_instance_key_survives_one_release():
+    """Two running instances with the same key (a copied ciphertext, a repeated document): the
+    first one's termination must not drop verdicts the second still reads, and a synchronous
+    miss after the last release still returns its verdict (no KeyError)."""
+    eng = FakeEngine()
+    ver = BatchVerifier(eng)
+    h = bytes([7]) * 8
+    ver.open_doc(h)
+    ver.open_doc(h)
+    ver.queue_sig(b"pk", h, b"\x02sh")
+    pending = ver.drain_async()
+    ver.release_doc(h)                   # instance A terminates while the drain is in flight
+    ver.commit(pending)
+    assert ver.sig_valid(b"pk", h, b"\x02sh") is True   # instance B: still cached
+    assert len(eng.calls) == 1
+    assert ver.sig_valid(b"pk2", h, b"\x03sh") is False  # B's miss: verified and cached
+    ver.release_doc(h)                   # B terminates: dropped
+    assert ver.cached() == 0
+    assert ver.sig_valid(b"pk3", h, b"\x04sh") is True   # a stray miss after release: no KeyError
+    assert ver.cached() == 0
+
+
+class FlowEngine(FakeEngine):
+    """FakeEngine plus a combine that always succeeds."""
+
+    def combine_verify_g2(self, t, idx, shares, master_pk, hashes):
+        return [b"S" * 192 for _ in idx], [0] * len(idx), b"\x01" * len(idx)
+
+
+def test_two_threshold_sign_instances_same_document():
+    """Two ThresholdSign instances on one document and one BatchVerifier: both terminate with
+    the reference's outputs and faults, whichever terminates first."""
+    from hbbft_amd.protocol import NetworkInfo, ThresholdSign
+    ver = BatchVerifier(FlowEngine())
+    n, t = 4, 1
+    pks = {i: bytes([i]) * 96 for i in range(n)}
+    ni = NetworkInfo(0, range(n), t, b"M" * 96, pks)       # observer: no secret key
+    a, b = ThresholdSign(ni, ver), ThresholdSign(ni, ver)
+    h = bytes([9]) * 192
+    a.set_document_hash(h)
+    b.set_document_hash(h)
+    for inst in (a, b):
+        inst.handle_input()
+        for j in range(n):
+            ver.queue_sig(pks[j], h, bytes([2 * j]) * 192)
+    ver.drain()
+    sa = a.handle_message(1, bytes([2]) * 192)
+    sa.extend(a.handle_message(2, bytes([4]) * 192))
+    assert a.terminated and sa.output == [b"S" * 192]
+    # b reads verdicts cached before a's release, then one that was never queued (a miss)
+    sb = b.handle_message(3, bytes([6]) * 192)
+    sb.extend(b.handle_message(2, bytes([5]) * 192))   # odd first byte: invalid -> fault
+    sb.extend(b.handle_message(1, bytes([2]) * 192))
+    assert b.terminated and sb.output == [b"S" * 192]
+    assert [f.kind for f in sb.fault_log] == ["UnverifiedSignatureShareSender"]
+    assert ver.cached() == 0

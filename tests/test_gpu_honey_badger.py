@@ -74,3 +74,25 @@ def test_epoch_n100_f33(engine):
     print("epoch N=100: %.3f s, %d engine calls, %d checks drained, %d consumed, timing %s" % (
         res.timing["epoch"], res.engine_calls, res.checks_gpu, res.checks_consumed,
         {k: round(v, 4) for k, v in res.timing.items()}))
+
+
+def test_failed_deferred_combine_is_replayed(engine):
+    """A combine that fails (here: the signing NetworkInfo's master key does not match the key
+    shares, so every combined signature fails PublicKey::verify) must surface as the reference's
+    Err(VerificationFailed) in the owning instance, which stays open (threshold_sign.rs:227-270),
+    not as an output.  The deferred epoch equals the immediate-combine epoch (defer=False)."""
+    n, t = 4, 1
+    rng = random.Random(404)
+    keys = NetworkKeys(engine, n, t, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=2, bad_every=5, proposal_bytes=80)
+    keys.master_pk = keys.pks[1]  # wrong master key: coins cannot verify; decryption is unaffected
+    dfr = run_epoch(engine, keys, trace, window=1 << 20)
+    imm = run_epoch(engine, keys, trace, window=1 << 20, defer=False)
+    assert dfr.coins == {} and dfr.signatures == {}
+    assert dfr.plaintexts == trace.proposals
+    assert {p for k, p, e in dfr.errors} == set(trace.coin_docs)
+    assert all(k == "coin" and e.kind == "VerificationFailed" for k, p, e in dfr.errors)
+    key = lambda r: (sorted((k, p, e.kind) for k, p, e in r.errors),
+                     sorted((k, p, f.node_id, f.kind) for k, p, f in r.faults))
+    assert key(dfr) == key(imm)
+    assert (imm.plaintexts, imm.coins) == (dfr.plaintexts, dfr.coins)

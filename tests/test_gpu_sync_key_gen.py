@@ -104,3 +104,115 @@ def test_sync_key_gen_faults(engine):
     outs = node.handle_acks([(0, good), (0, good), (3, bad)])
     assert outs[0].valid and outs[1].valid and outs[2].fault == "ValueCommitment"
     assert node.parts[0].acks == {0, 3} and list(node.parts[0].values) == [1]
+
+
+def test_multiple_parts_after_ack(engine):
+    """ProposalState's derived PartialEq covers values and acks (sync_key_gen.rs:254-262, 489-493):
+    an identical Part re-sent after an Ack for that proposer is MultipleParts, not Valid(None)."""
+    n, t = 4, 1
+    rng = random.Random(78)
+    nodes, props = make_nodes(engine, n, t, rng)
+    node = nodes[1]
+    assert node.handle_part(0, props[0], rng).ack is not None
+    again = node.handle_part(0, props[0], rng)
+    assert again.valid and again.ack is None          # no Ack yet: the same Part is ignored
+    ack = nodes[2].handle_part(0, props[0], rng).ack
+    assert node.handle_ack(2, ack).valid
+    assert node.handle_part(0, props[0], rng).fault == "MultipleParts"
+    # an observer records acks too (without values): the same rule holds for it
+    obs, _ = SyncKeyGen.new(99, 5, nodes[0].pub_keys, t, engine, rng=rng)
+    assert obs.handle_part(0, props[0], rng).valid
+    assert obs.handle_ack(2, ack).valid
+    assert obs.handle_part(0, props[0], rng).fault == "MultipleParts"
+
+
+def _ack_with_payload(kg, ack, our_idx, payload, rng):
+    """``ack`` with the value encrypted to node ``our_idx`` replaced by ``payload``."""
+    from hbbft_amd.sync_key_gen import _encrypt_batch
+    vals = list(ack.values)
+    vals[our_idx] = _encrypt_batch([kg.pub_keys[our_idx]], [payload], rng)[0]
+    return Ack(ack.proposer_idx, vals)
+
+
+def test_ack_value_faults(engine):
+    """AckFault::DecryptValue / DeserializeValue (sync_key_gen.rs:535-541): a tampered ciphertext
+    fails Ciphertext::verify; a payload that is not a bincode FieldWrap<Fr> (too short, or >= r)
+    does not deserialise.  bincode 1.x ignores trailing bytes, so a 33-byte payload whose first
+    32 bytes are the right value is Valid.  The sender's ack is recorded in every case (:527)."""
+    from hbbft_amd.sync_key_gen import _decrypt_batch
+    n, t = 4, 1
+    rng = random.Random(79)
+    nodes, props = make_nodes(engine, n, t, rng)
+    node = nodes[1]
+    acks = {j: nodes[j].handle_part(0, props[0], rng).ack for j in range(n)}  # node 1 handles part 0 too
+    # DecryptValue: our value's W swapped for another ciphertext's
+    vals = list(acks[0].values)
+    vals[1] = Ciphertext(vals[1].u, vals[1].v, vals[0].w)
+    assert node.handle_ack(0, Ack(0, vals)).fault == "DecryptValue"
+    # DeserializeValue: 31 bytes; a value >= r
+    out = node.handle_ack(2, _ack_with_payload(nodes[2], acks[2], 1, b"\x01" * 31, rng))
+    assert out.fault == "DeserializeValue"
+    out = node.handle_ack(3, _ack_with_payload(nodes[3], acks[3], 1, (R_ORDER + 5).to_bytes(32, "little"), rng))
+    assert out.fault == "DeserializeValue"
+    assert node.parts[0].acks == {0, 2, 3} and node.parts[0].values == {}
+    # 33 bytes = the right value + one trailing byte: Valid
+    v1 = _decrypt_batch(engine, node.sec_key, [acks[1].values[1]])[0]
+    assert len(v1) == 32
+    out = node.handle_ack(1, _ack_with_payload(nodes[1], acks[1], 1, v1 + b"\x07", rng))
+    assert out.valid and list(node.parts[0].values) == [2]
+
+
+def test_part_row_faults(engine):
+    """PartFault::DeserializeRow (sync_key_gen.rs:507) for a row payload that is not a bincode Poly
+    (truncated, or a coefficient >= r); a well-formed row with the wrong coefficient count
+    deserialises and fails the commitment comparison (RowCommitment, :508-510)."""
+    from hbbft_amd.sync_key_gen import _encrypt_batch, ser_row
+    n, t = 4, 1
+    rng = random.Random(80)
+    nodes, props = make_nodes(engine, n, t, rng)
+    node = nodes[1]
+    pk1 = node.pub_keys[1]
+
+    def with_row(part, payload):
+        rows = list(part.rows)
+        rows[1] = _encrypt_batch([pk1], [payload], rng)[0]
+        return Part(part.degree, part.commit, rows)
+
+    good_row = [3] * (t + 1)
+    assert node.handle_part(0, with_row(props[0], ser_row(good_row)[:-1]), rng).fault == "DeserializeRow"
+    assert node.handle_part(2, with_row(props[2], ser_row([R_ORDER] + [1] * t)), rng).fault == "DeserializeRow"
+    assert node.handle_part(3, with_row(props[3], ser_row([1] * (t + 2))), rng).fault == "RowCommitment"
+    # each was recorded (the state is inserted before the row is checked): a re-send is Valid(None)
+    assert set(node.parts) == {0, 2, 3}
+
+
+def test_mixed_degree_parts(engine):
+    """Parts of another degree are valid in the reference (row / evaluate run at the part's own
+    degree); a batch mixing degrees runs one engine call per degree and equals one-by-one handling;
+    generate() adds row(0) commitments of different lengths (Commitment's AddAssign resizes)."""
+    n, t = 4, 1
+    rng = random.Random(81)
+    sks = [rng.randrange(1, R_ORDER) for _ in range(n)]
+    pub = dict(enumerate(hoststage.g1_mul([G1_GEN] * n, sks)))
+    nodes, props = [], []
+    for i in range(n):
+        kg, part = SyncKeyGen.new(i, sks[i], pub, t + (i == 2), engine, rng=rng)  # node 2 proposes degree 2
+        kg.threshold = t
+        nodes.append(kg)
+        props.append(part)
+    assert props[2].degree == t + 1 and len(props[2].commit) == 6
+    outs = nodes[0].handle_parts([(p, props[p]) for p in range(n)], rng)
+    assert all(o.valid and o.ack is not None for o in outs)
+    acks = [[] for _ in range(n)]
+    for j, kg in enumerate(nodes):
+        for p in range(n):
+            o = kg.handle_part(p, props[p], rng) if j else None
+            if j:
+                assert o.valid and o.ack is not None
+                acks[p].append((j, o.ack))
+    acks_all = [a for p in range(n) for a in acks[p]] + [(0, o.ack) for o in outs]
+    res = nodes[0].handle_acks(acks_all)
+    assert all(r.valid for r in res)
+    assert all(nodes[0].parts[p].is_complete(t) for p in range(n))
+    pks, sk = nodes[0].generate()
+    assert len(pks.commit) == t + 2  # degree-2 part's row(0) extends the key's commitment

@@ -4,6 +4,8 @@ from oracle import bls12_381 as C
 from oracle import tc
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
 from hbbft_amd.protocol import Fault, Step, g1_compress_abi, xor_with_hash
+import hbbft_amd.sync_key_gen as skg
+import pytest
 
 
 def test_compress_and_xor_stream_match_oracle():
@@ -40,3 +42,12 @@ def test_uncompressed_flag_and_field_checks():
             g1_abi_from_uncompressed(bad)
     with pytest.raises(ValueError):
         g2_abi_from_uncompressed(g2[:96] + P_FIELD.to_bytes(48, "big") + g2[144:])
+
+
+def test_malformed_commitment_rejected():
+    """A BivarCommitment whose point count does not match its degree cannot be built (it would
+    misalign every other part of a batched engine call)."""
+    with pytest.raises(ValueError):
+        skg.Part(2, [bytes(96)] * 5, [])
+    with pytest.raises(ValueError):
+        skg.Part(1, [bytes(96)] * 4, [])
