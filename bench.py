@@ -64,8 +64,80 @@ def log(*a):
 
 def dist_backend():
     """nccl (= RCCL) by default; HBH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks then
-    share devices round-robin and the timing reduction runs on host tensors)."""
-    return os.environ.get("HBH_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+    share devices round-robin and the timing reduction runs on host tensors).  Decided from the
+    device COUNT, which does not initialise the GPU runtime (a parent that spawns the ranks must
+    not)."""
+    return os.environ.get("HBH_DIST_BACKEND", "nccl" if torch.cuda.device_count() > 0 else "gloo")
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def pool_devices(n):
+    """Devices of the --launcher pool shards: 0..n-1, or HBH_POOL_DEVICES (e.g. "0,0" runs two
+    shards on device 0, the one-GPU rehearsal of the pool path)."""
+    env = os.environ.get("HBH_POOL_DEVICES")
+    devs = [int(x) for x in env.split(",") if x.strip()] if env else list(range(n))
+    if len(devs) != n:
+        raise SystemExit("bench.py: HBH_POOL_DEVICES lists %d devices, --gpus %d" % (len(devs), n))
+    return devs
+
+
+def launch(args):
+    """Honour --gpus N.  Returns None when this process should run the benchmark itself, else the
+    exit code to leave with:
+      * under torchrun (WORLD_SIZE set): WORLD_SIZE must equal --gpus and, on RCCL, that many
+        devices must be visible;
+      * --gpus N > 1 without WORLD_SIZE, --launcher ranks (default): spawn N ranks with
+        torch.distributed.run as a CHILD process (this process has not touched the GPU) and return
+        its exit code;
+      * --launcher pool: one process drives the in-ABI engine pool over N devices;
+    fewer visible devices than asked for is an error (exit 2), never a silent 1-GPU run."""
+    visible = torch.cuda.device_count()
+    # HBH_DIST_BACKEND=gloo explicitly: rehearse N ranks sharing the visible device(s)
+    need = 1 if os.environ.get("HBH_DIST_BACKEND") == "gloo" else args.gpus
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None:
+        if int(env) != args.gpus:
+            log("bench.py: WORLD_SIZE=%s but --gpus %d" % (env, args.gpus))
+            return 2
+        if visible < need:
+            log("bench.py: %d ranks need %d devices, %d visible" % (args.gpus, need, visible))
+            return 2
+        return None
+    if args.gpus < 1:
+        return 2
+    if args.launcher == "pool":
+        devs = pool_devices(args.gpus)
+        if visible < 1 or max(devs) >= visible:
+            log("bench.py: pool devices %s, %d visible" % (devs, visible))
+            return 2
+        return None
+    if visible < need:
+        log("bench.py: --gpus %d but %d devices visible" % (args.gpus, visible))
+        return 2
+    if args.gpus == 1:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench.py: spawning %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd)
+
+
+def gather_per_rank(value, world):
+    """Every rank's value on every rank (reporting only: per-rank kernel times)."""
+    if world == 1:
+        return [value]
+    out = [None] * world
+    dist.all_gather_object(out, value)
+    return out
 
 
 def rank_device(local):
@@ -175,10 +247,13 @@ def pair_waves_per_simd(checks):
 
 
 def cpu_info():
+    """(nproc, affinity CPUs, threads the CPU baseline uses).  The thread count is the host stage's
+    own detection (hbh_host_threads: affinity mask, cgroup cpu.max quota, HBH_HOST_THREADS /
+    OMP_NUM_THREADS -- 16 on the GPU box, one GPU's share of the host)."""
+    from hbbft_amd import hoststage
     ncpu = os.cpu_count() or 1
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else ncpu
-    # one GPU's share of the host on the GPU pool is 16 threads (box policy); never more than affinity
-    return ncpu, aff, max(1, min(aff, 16))
+    return ncpu, aff, max(1, hoststage.host_threads())
 
 
 def timed_pool(fn, items, threads):
@@ -231,9 +306,8 @@ def cpu_baseline(w, budget_s=12.0):
                       "C restatement of pairing 0.14 (two pairings per check)" % (n2, threads, n1, n1 / st),
             "single_thread_value": n1 / st, "combine_latency_ms": comb_ms,
             "nproc": ncpu, "affinity": aff,
-            "all_cores_linear_estimate": n1 / st * ncpu,
-            "cores_note": "measured on the GPU box's CPU share (%d threads); all_cores_linear_estimate = "
-                          "single-thread rate x nproc (%d), an upper bound" % (threads, ncpu)}
+            "cores_note": "measured on %d threads = the CPUs this process may use (hbh_host_threads: affinity, "
+                          "cgroup quota, OMP_NUM_THREADS); nproc %d counts the whole machine" % (threads, ncpu)}
 
 
 def pmc_traffic(kernel):
@@ -329,12 +403,20 @@ def main():
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="epoch workload: drain each window before handling it (no GPU/host overlap)")
+    ap.add_argument("--launcher", choices=["ranks", "pool"], default="ranks",
+                    help="--gpus N > 1 without torchrun: spawn N ranks (one process per GPU, default) or drive "
+                         "the in-ABI engine pool (hbh_pool_*) over N devices from this process")
     ap.add_argument("--workload", choices=["sign", "decrypt", "dkg", "epoch"], default="sign",
                     help="sign = BASELINE configs[1] (default, the headline metric); decrypt = configs[2] "
                          "(64k decryption-share checks + G1 combines, strong-scaled over ranks); dkg = configs[3] "
                          "(SyncKeyGen N=100 t=33 ack checks of one node); epoch = configs[4] (HoneyBadger N=100 f=33 "
                          "epoch crypto of one node)")
     args = ap.parse_args()
+    rc = launch(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.launcher == "pool" and "WORLD_SIZE" not in os.environ:
+        return run_pool(args)
     if args.workload != "sign":
         return run_other(args)
 
@@ -375,8 +457,8 @@ def main():
                                   d_di.data_ptr(), None, d_sg.data_ptr(), n, None,
                                   d_vs[k % len(streams)].data_ptr())   # P2 = g1 (flag)
 
-    def verdicts_ok():
-        return all(bool((d.cpu().numpy() == w.expected).all()) for d in d_vs)
+    def verdicts_ok(nbuf=None):
+        return all(bool((d.cpu().numpy() == w.expected).all()) for d in d_vs[:nbuf])
 
     for k in range(len(streams)):
         step(k)
@@ -386,9 +468,12 @@ def main():
         raise SystemExit("verdict mismatch against the construction")
     for k in range(args.warmup):
         step(k)
+    torch.cuda.synchronize(dev)
+    for d in d_vs:      # the timed steps must write every verdict again
+        d.zero_()
     ms_step = timed_steps(step, streams, args.steps, world, dev)
     value = n * world / (ms_step / 1e3)
-    ok = ok and verdicts_ok()
+    ok = ok and verdicts_ok(min(args.steps, len(streams)))
     # roofline: isolated launches on one stream (no overlap), HIP events around each launch
     eng.set_profiling(True)
     for _ in range(max(2, min(args.steps, 5))):
@@ -398,6 +483,9 @@ def main():
     prep_ms, prep_n = eng.stage_time(STAGE_PREPARE)
     eng.set_profiling(False)
     ok = ok and verdicts_ok()
+    per_rank = gather_per_rank({"rank": rank, "device": local, "kernel_ms": pair_ms / max(pair_n, 1),
+                                "ms_per_step": ms_step, "verdicts_ok": ok}, world)
+    ok = all(r["verdicts_ok"] for r in per_rank)
 
     if rank == 0:
         kern_ms = pair_ms / max(pair_n, 1)
@@ -417,7 +505,7 @@ def main():
                        "streams": len(streams),
                        "documents_per_gpu": nh, "n_nodes": N_NODES, "f": F_FAULTY, "pairing_impl": args.impl,
                        "parallelism": "shard-by-batch x%d" % world},
-            "verdicts_ok": ok,
+            "verdicts_ok": ok, "per_rank": per_rank,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
                              traffic=pmc_traffic(KERNEL_NAMES[args.impl]), kernels=kernels,
                              note="achieved = checks x algorithmic MADs per check (workcount.PAIR_CHECK_WALK: "
@@ -499,8 +587,8 @@ def run_decrypt(args, eng, world, rank, dev):
                                   d_ci.data_ptr(), d_pk.data_ptr(), d_w.data_ptr(), len(mine), d_ci.data_ptr(),
                                   d_vs[k % len(streams)].data_ptr())
 
-    def verdicts_ok():
-        return all(bool((d.cpu().numpy()[:n] == expected).all()) for d in d_vs)
+    def verdicts_ok(nbuf=None):
+        return all(bool((d.cpu().numpy()[:n] == expected).all()) for d in d_vs[:nbuf])
 
     for k in range(len(streams)):
         step(k)
@@ -508,7 +596,11 @@ def run_decrypt(args, eng, world, rank, dev):
     ok = verdicts_ok()
     for k in range(args.warmup):
         step(k)
+    torch.cuda.synchronize(dev)
+    for d in d_vs:      # the timed steps must write every verdict again
+        d.zero_()
     ms_step = timed_steps(step, streams, args.steps, world, dev)
+    ok = ok and verdicts_ok(min(args.steps, len(streams)))
     from hbbft_amd._lib import STAGE_PAIRING, STAGE_PREPARE
     eng.set_profiling(True)   # roofline: isolated single-stream launches
     for _ in range(max(2, min(args.steps, 5))):
@@ -535,6 +627,9 @@ def run_decrypt(args, eng, world, rank, dev):
     eng.set_profiling(False)
     want = eng.g1_mul(us, [coeffs[0]] * len(mine))
     ok = ok and out == want and all(x == 0 for x in st)
+    per_rank = gather_per_rank({"rank": rank, "checks": n, "ciphertexts": len(mine),
+                                "kernel_ms": pair_ms / max(pair_n, 1), "ms_per_step": ms_step, "ok": ok}, world)
+    ok = all(r["ok"] for r in per_rank)
     if rank == 0:
         main_k = roofline_entry("hbs::k_pair_verify<false, false, 0>", pair_n, pair_ms / max(pair_n, 1), n,
                                 workcount.PAIR_CHECK_TABLE, "decryption-share check", pair_waves_per_simd(n))
@@ -550,7 +645,7 @@ def run_decrypt(args, eng, world, rank, dev):
             "data": "synthetic, seeded (H_uv synthetic in G2; 1/64 invalid shares)",
             "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total, "streams": len(streams),
                        "ciphertexts": ncts, "parallelism": "shard-by-ciphertext x%d" % world},
-            "verdicts_ok": ok, "combines_ok": out == want,
+            "verdicts_ok": ok, "combines_ok": out == want, "per_rank": per_rank,
             "combines_per_s_rank0": len(mine) / comb_s,                 # host-to-host, one call
             "combines_per_s_rank0_device": len(mine) / (comb_dev_ms / 1e3),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
@@ -588,8 +683,7 @@ def cpu_baseline_decrypt(shares, pks, huv, ws, us, inst, expected, cidx, cpts, m
     return {"value": n2 / mt, "unit": "shares/s", "cores": threads, "kind": "port",
             "sample": "%d decryption-share checks on %d threads (%d on 1 thread: %.1f shares/s); C restatement of "
                       "pairing 0.14, two pairings per check" % (n2, threads, n1, n1 / st),
-            "single_thread_value": n1 / st, "combine_g1_ms": comb_ms, "nproc": ncpu, "affinity": aff,
-            "all_cores_linear_estimate": n1 / st * ncpu}
+            "single_thread_value": n1 / st, "combine_g1_ms": comb_ms, "nproc": ncpu, "affinity": aff}
 
 
 def run_dkg(args, eng, world, rank, dev):
@@ -648,6 +742,9 @@ def run_dkg(args, eng, world, rank, dev):
     dev_ms /= max(dev_n, 1)
     ms = _max_over_ranks(dev_ms, world, dev)
     host_ms = _max_over_ranks(statistics.median(times), world, dev)
+    per_rank = gather_per_rank({"rank": rank, "device_ms": dev_ms, "host_ms": statistics.median(times), "ok": ok},
+                               world)
+    ok = all(r["ok"] for r in per_rank)
     if rank == 0:
         nack = len(vals)
         ops = [workcount.bivar_ack(t, y) for y in ys]
@@ -663,7 +760,7 @@ def run_dkg(args, eng, world, rank, dev):
                        "parts": n_nodes, "commitment_points": npos, "parallelism": "one node per rank x%d" % world,
                        "timing": "device time of the row + check kernels (HIP events); host_to_host_ms includes "
                                  "the 5.7 MB commitment upload"},
-            "host_to_host_ms": host_ms, "verdicts_ok": ok,
+            "host_to_host_ms": host_ms, "verdicts_ok": ok, "per_rank": per_rank,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
                              traffic=pmc_traffic("hbs::k_bivar_check_quad"),
                              note="four lanes per ack (lane quads), 10,000 acks = 625 waves: latency-bound at "
@@ -693,8 +790,7 @@ def cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, g1, per_thread=16):
     return {"value": n2 / mt, "unit": "acks/s", "cores": threads, "kind": "port",
             "sample": "%d ack checks on %d threads (%d on 1 thread: %.1f acks/s); C restatement of "
                       "BivarCommitment::evaluate + G1 scalar multiplication" % (n2, threads, n1, n1 / st),
-            "single_thread_value": n1 / st, "nproc": ncpu, "affinity": aff,
-            "all_cores_linear_estimate": n1 / st * ncpu}
+            "single_thread_value": n1 / st, "nproc": ncpu, "affinity": aff}
 
 
 def run_epoch_bench(args, eng, world, rank, dev):
@@ -792,8 +888,105 @@ def cpu_baseline_epoch(eng, keys, tr, res, sample=12):
                       "epoch's %d consumed checks, %d coins, %d decryptions (a HoneyBadger node handles its "
                       "messages on one thread)" % (len(items), res.checks_consumed, ncoin, nct),
             "epoch_ms": epoch_s * 1e3, "per_check_ms": per_check * 1e3, "combine_g2_ms": comb_g2 * 1e3,
-            "combine_g1_ms": comb_g1 * 1e3, "nproc": ncpu, "affinity": aff,
-            "all_cores_linear_estimate": ncpu / epoch_s}
+            "combine_g1_ms": comb_g1 * 1e3, "nproc": ncpu, "affinity": aff}
+
+
+def run_pool(args):
+    """--launcher pool: ONE process drives the in-ABI engine pool (hbh_pool_*, csrc/pool.cpp) over
+    --gpus N shards (devices 0..N-1, or HBH_POOL_DEVICES).  Weak scaling like the ranks path: the
+    batch is N x --batch checks over N x the documents (each shard's slice = one configs[1] batch),
+    split by instance inside the pool, one host thread and stream per shard, verdicts gathered in
+    order.  The pool's entry points take HOST buffers, so a step here is host-to-host (the PCIe
+    upload of 288 B per check and the verdict download included); the per-shard kernel times are
+    the engines' HIP-event times.  Workloads: sign, decrypt (1,024 x N ciphertexts)."""
+    import ctypes
+    from hbbft_amd import workcount
+    from hbbft_amd._lib import STAGE_PAIRING, buf, check
+    from hbbft_amd.engine import Engine, Pool
+    if args.workload not in ("sign", "decrypt"):
+        raise SystemExit("bench.py: --launcher pool runs the sign and decrypt workloads")
+    devs = pool_devices(args.gpus)
+    nsh = len(devs)
+    gen = Engine(devs[0])
+    n = args.batch
+    w = Workload(gen, n, seed=20261016)
+    nh = len(w.hashes)
+    total = n * nsh
+    di = np.ascontiguousarray(np.concatenate([w.doc_idx + s * nh for s in range(nsh)]).astype(np.uint32))
+    expected = np.tile(w.expected, nsh)
+    if args.workload == "sign":
+        ins = [w.pk_batch * nsh, w.sig_batch * nsh, w.hash_table * nsh]
+        fn_name, kernel, op, unit_name = ("hbh_verify_sig_shares", KERNEL_NAMES["pair"], workcount.PAIR_CHECK_WALK,
+                                          "share check")
+    else:
+        # decryption shares with the sign batch's layout: D_i = U_c * sk_i, H_uv / W per ciphertext
+        rng = random.Random(4243)
+        rs = [rng.randrange(1, R_ORDER) for _ in range(nh)]
+        us = gen.g1_mul([w.g1] * nh, rs)
+        ws = gen.g2_mul(w.hashes, rs)                                              # W = H_uv r
+        bad = np.nonzero(w.expected == 0)[0]
+        dsh = gen.g1_mul([us[w.doc_idx[i]] for i in range(n)],
+                         [rng.randrange(1, R_ORDER) if i in set(bad) else w.sk[w.node[i]] for i in range(n)])
+        ins = [b"".join(dsh) * nsh, w.pk_batch * nsh, w.hash_table * nsh, b"".join(ws) * nsh]
+        fn_name, kernel, op, unit_name = ("hbh_verify_dec_shares", "hbs::k_pair_verify<false, false, 0>",
+                                          workcount.PAIR_CHECK_TABLE, "decryption-share check")
+    gen.close()
+    pool = Pool(devs)
+    pool.set_pairing_impl(IMPLS[args.impl])
+    keep = [buf(b) for b in ins]
+    out = (ctypes.c_uint8 * total)()
+    pout = ctypes.cast(out, ctypes.c_void_p)
+    pdi = di.ctypes.data_as(ctypes.c_void_p)
+    fn = getattr(pool._l, fn_name)
+
+    def step():
+        ptrs = [k[1] for k in keep]
+        if args.workload == "sign":
+            check(fn(pool._h, total, ptrs[0], ptrs[1], ptrs[2], nh * nsh, pdi, pout))
+        else:
+            check(fn(pool._h, total, ptrs[0], ptrs[1], ptrs[2], ptrs[3], nh * nsh, pdi, pout))
+
+    def verdicts_ok():
+        return bool((np.frombuffer(bytes(out), dtype=np.uint8) == expected).all())
+
+    step()
+    ok = verdicts_ok()
+    for _ in range(args.warmup):
+        step()
+    ctypes.memset(out, 0, total)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ms_step = (time.perf_counter() - t0) * 1e3 / args.steps
+    ok = ok and verdicts_ok()
+    engines = [pool.shard_engine(s) for s in range(nsh)]
+    for e in engines:
+        e.set_profiling(True)
+    step()
+    per_shard = []
+    for s, e in enumerate(engines):
+        ms, nl = e.stage_time(STAGE_PAIRING)
+        per_shard.append({"shard": s, "device": devs[s], "kernel_ms": ms / max(nl, 1), "launches": nl})
+        e.set_profiling(False)
+    ok = ok and verdicts_ok()
+    kern = max(p["kernel_ms"] for p in per_shard)
+    main_k = roofline_entry(kernel, 1, kern, n, op, unit_name, pair_waves_per_simd(n))
+    metric = METRIC if args.workload == "sign" else "verified decryption shares/sec (whole node), N=64 f=21"
+    line = {
+        "metric": metric, "value": total / (ms_step / 1e3), "unit": "shares/s", "n_gpus": len(set(devs)),
+        "shards": nsh, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
+        "data": "synthetic, seeded (one configs[1] batch per shard; 1/64 invalid)",
+        "config": {"workload": "%s through the engine pool, BASELINE configs[1]/[2]" % args.workload,
+                   "batch_per_shard": n, "documents_per_shard": nh, "devices": devs,
+                   "parallelism": "engine pool, shard-by-instance x%d" % nsh,
+                   "timing": "host-to-host pool calls (PCIe upload + verdict gather included)"},
+        "verdicts_ok": ok, "per_shard": per_shard,
+        "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
+                         note="slowest shard's kernel time (HIP events on the shard's stream)"),
+    }
+    print(json.dumps(line), flush=True)
+    pool.close()
 
 
 def run_other(args):

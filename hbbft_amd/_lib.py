@@ -63,6 +63,7 @@ SIGNATURES = [
     ("hbh_pool_bivar_ack_check", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P, _P, _P]),
     # host stage (no engine, no GPU)
     ("hbh_host_last_error", _c.c_char_p, []),
+    ("hbh_host_threads", _I, [_c.POINTER(_I)]),
     ("hbh_hash_g2", _I, [_SZ, _P, _P, _P, _I]),
     ("hbh_hash_g1_g2", _I, [_SZ, _P, _P, _P, _P, _I]),
     ("hbh_xor_with_hash", _I, [_SZ, _P, _P, _P, _P, _I]),

@@ -427,6 +427,12 @@ int hbh_xor_with_hash(size_t n, const uint8_t* g, const uint8_t* data, const siz
   return HBH_OK;
 }
 
+int hbh_host_threads(int* out) {
+  if (!out) return host_fail(HBH_ERR_ARG, "null pointer");
+  *out = (int)hh::usable_cpus();
+  return HBH_OK;
+}
+
 int hbh_signature_parity(size_t n, const uint8_t* sigs, uint8_t* out) {
   if (n == 0) return HBH_OK;
   if (!sigs || !out) return host_fail(HBH_ERR_ARG, "null pointer");

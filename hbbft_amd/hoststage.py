@@ -72,6 +72,14 @@ def xor_with_hash(gs, datas, threads=0):
     return [raw[int(offs[i]):int(offs[i + 1])] for i in range(n)]
 
 
+def host_threads():
+    """Workers the host stage uses for threads=0: the CPUs this process may use (affinity,
+    cgroup cpu.max quota, HBH_HOST_THREADS / OMP_NUM_THREADS; hbh_host_threads)."""
+    n = ctypes.c_int()
+    check_host(_lib.lib().hbh_host_threads(ctypes.byref(n)))
+    return n.value
+
+
 def signature_parity(sigs):
     """Signature::parity per G2 point (the BA coin value, binary_agreement.rs:402)."""
     l = _lib.lib()

@@ -247,8 +247,11 @@ int hbh_g2_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out
  *   hbh_encrypt       PublicKey::encrypt_with_rng with caller-drawn Fr nonces (32 B LE each):
  *                     U = g1 r, V = msg xor stream(pk r), W = hash_g1_g2(U, V) r
  *                     (sync_key_gen.rs:346-357,386-390; honey_badger/epoch_state.rs:224-237);
- *                     pks holds one key, or one per item when pk_per_item != 0 */
+ *                     pks holds one key, or one per item when pk_per_item != 0
+ *   hbh_host_threads  the worker count `threads` = 0 means: the CPUs this process may use
+ *                     (affinity mask, cgroup v2 cpu.max quota, HBH_HOST_THREADS / OMP_NUM_THREADS) */
 const char* hbh_host_last_error(void);
+int hbh_host_threads(int* out);
 int hbh_hash_g2(size_t n, const uint8_t* data, const size_t* offsets, uint8_t* out, int threads);
 int hbh_hash_g1_g2(size_t n, const uint8_t* u, const uint8_t* data, const size_t* offsets, uint8_t* out,
                    int threads);

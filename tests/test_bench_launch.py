@@ -1,0 +1,63 @@
+"""bench.py honours --gpus N: never a silent one-GPU run.
+
+CPU: too few visible devices, a WORLD_SIZE that disagrees with --gpus and a pool over absent
+devices all exit non-zero before any GPU work.  GPU (one MI355X): the pool path with two shards
+on device 0 and the spawned-ranks path with two ranks rehearsed on device 0 (gloo) both report
+their shards / ranks and exact verdicts."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra, timeout=120):
+    env = dict(os.environ)
+    env.update(env_extra)
+    return subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_too_few_devices_exits_nonzero():
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
+    assert r.returncode != 0 and "devices visible" in r.stderr
+    assert not r.stdout.strip()
+
+
+def test_world_size_must_match_gpus():
+    r = _run(["--gpus", "2", "--steps", "1"], {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=4" in r.stderr
+
+
+def test_pool_over_absent_devices_exits_nonzero():
+    r = _run(["--gpus", "2", "--launcher", "pool"], {"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
+    assert r.returncode == 2
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_pool_bench_two_shards_on_device0():
+    r = _run(["--gpus", "2", "--launcher", "pool", "--batch", "4096", "--steps", "2", "--warmup", "1"],
+             {"HBH_POOL_DEVICES": "0,0"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["verdicts_ok"] is True
+    assert d["shards"] == 2 and d["n_gpus"] == 1 and len(d["per_shard"]) == 2
+    assert all(p["launches"] >= 1 and p["kernel_ms"] > 0 for p in d["per_shard"])
+
+
+@pytest.mark.gpu
+def test_spawned_ranks_rehearsed_on_device0():
+    r = _run(["--gpus", "2", "--batch", "4096", "--steps", "2", "--warmup", "1", "--no-combine",
+              "--no-cpu-baseline"], {"HBH_DIST_BACKEND": "gloo"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["verdicts_ok"] is True and len(d["per_rank"]) == 2
