@@ -63,27 +63,51 @@ HS_MULFN Fp h_mul_l(HS_P14(x), HS_P14(y)) {
   int32_t m[NL];
   int64_t acc = 0;
   Fp r;
+  // HS_NCH > 1: the Z W terms and the reduction terms run in a second chain (sfp.hpp)
 #pragma unroll
   for (int k = 0; k < NL; k++) {
+    int64_t c2 = 0;
 #pragma unroll
     for (int i = 0; i <= k; i++) {
       acc += (int64_t)a.l[i] * Y[k - i];
-      acc += (int64_t)Z[i] * W[k - i];
+      if (HS_NCH > 1) {
+        c2 += (int64_t)Z[i] * W[k - i];
+        HS_CHAIN(c2);
+      } else {
+        acc += (int64_t)Z[i] * W[k - i];
+      }
     }
 #pragma unroll
-    for (int i = 0; i < k; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+    for (int i = 0; i < k; i++) {
+      if (HS_NCH > 1) {
+        c2 += (int64_t)m[i] * (int32_t)P_L[k - i];
+        HS_CHAIN(c2);
+      } else {
+        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+      }
+    }
+    if (HS_NCH > 1) acc += c2;
     m[k] = (int32_t)(((uint32_t)acc * NP0) & (uint32_t)MASK28);
     acc += (int64_t)m[k] * (int32_t)P_L[0];
     acc >>= 28;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
+    int64_t c2 = 0;
 #pragma unroll
     for (int i = k - NL + 1; i < NL; i++) {
       acc += (int64_t)a.l[i] * Y[k - i];
-      acc += (int64_t)Z[i] * W[k - i];
-      acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+      if (HS_NCH > 1) {
+        c2 += (int64_t)Z[i] * W[k - i];
+        HS_CHAIN(c2);
+        c2 += (int64_t)m[i] * (int32_t)P_L[k - i];
+        HS_CHAIN(c2);
+      } else {
+        acc += (int64_t)Z[i] * W[k - i];
+        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+      }
     }
+    if (HS_NCH > 1) acc += c2;
     r.l[k - NL] = (int32_t)acc & MASK28;
     acc >>= 28;
   }

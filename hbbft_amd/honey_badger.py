@@ -30,8 +30,9 @@ import sys
 import time
 
 from . import hoststage
-from .protocol import BatchVerifier, Ciphertext, Deferred, NetworkInfo, ProtocolError, Step, ThresholdDecrypt, \
-    ThresholdSign, signature_parity
+from . import wire
+from .protocol import BatchVerifier, Ciphertext, Deferred, Fault, NetworkInfo, ProtocolError, Step, \
+    ThresholdDecrypt, ThresholdSign, signature_parity
 from .sync_key_gen import G1_GEN, R_ORDER
 
 __all__ = ["NetworkKeys", "EpochTrace", "coin_document", "run_epoch", "EpochResult"]
@@ -125,6 +126,29 @@ class EpochTrace:
         return tr
 
 
+def _serialize(trace, corrupt=()):
+    """Attach the bincode bytes node ``our`` receives (hbbft_amd.wire): raw_coin / raw_dec per
+    (proposer, sender) share message, raw_cts per contribution.  ``corrupt``: keys
+    ("coin" | "dec", p, j) or ("ct", p) whose bytes are damaged (test use)."""
+    ck = sorted(trace.coin_shares)
+    dk = sorted(trace.dec_shares)
+    trace.raw_coin = dict(zip(ck, wire.encode_sig_share_msgs([trace.coin_shares[k] for k in ck])))
+    trace.raw_dec = dict(zip(dk, wire.encode_dec_share_msgs([trace.dec_shares[k] for k in dk])))
+    ps = sorted(trace.cts)
+    trace.raw_cts = dict(zip(ps, wire.encode_ciphertexts([trace.cts[p] for p in ps])))
+    for c in corrupt:
+        if c[0] == "ct":
+            b = trace.raw_cts[c[1]]
+            trace.raw_cts[c[1]] = b[:8] + bytes([b[8] ^ 0x01]) + b[9:]  # a compressed x that is not on the curve
+        else:
+            d = trace.raw_coin if c[0] == "coin" else trace.raw_dec
+            d[(c[1], c[2])] = d[(c[1], c[2])][:-1]                      # truncated
+    return trace
+
+
+EpochTrace.serialize = _serialize
+
+
 class EpochResult:
     def __init__(self):
         self.coins = {}        # proposer -> bool (signature parity)
@@ -139,7 +163,7 @@ class EpochResult:
         self.combines = 0
 
 
-def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelined=True, limit=None):
+def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelined=True, limit=None, decode=None):
     """Deliver msgs in windows: queue the checks of messages whose instance is still running,
     drain once, then hand every message to its instance.
 
@@ -150,7 +174,11 @@ def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelin
 
     limit: pre-verify at most this many shares per instance (threshold + slack); a share the
     instance still reads after that is a cache miss, verified on its own (BatchVerifier.*_valid)
-    -- same verdicts, fewer checks drained for instances that terminate early."""
+    -- same verdicts, fewer checks drained for instances that terminate early.
+
+    decode: raw-message mode -- decode(batch) turns a window's message bytes into share points in
+    one batched call (hbbft_amd.wire) before the window is queued; a message that does not decode
+    is dropped and logged as a ``DeserializeMessage`` fault of its sender."""
     def hand(batch):
         for p, j in batch:
             try:
@@ -162,13 +190,19 @@ def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelin
             if step.output:
                 yield p, step.output[0]
 
-    yield from _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, {})
+    yield from _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, {}, decode, res, kind)
 
 
-def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, queued):
+def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, queued, decode=None, res=None,
+             kind=None):
     prev = None
     for w0 in range(0, len(msgs), window):
         batch = msgs[w0:w0 + window]
+        if decode is not None:
+            bad = decode(batch)
+            if bad:
+                res.faults += [(kind, p, Fault(j, "DeserializeMessage")) for p, j in batch if (p, j) in bad]
+                batch = [m for m in batch if m not in bad]
         for p, j in batch:
             if not instance[p].terminated:
                 c = queued.get(p, 0)
@@ -189,7 +223,7 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
 
 
 def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True, slack=4, switch_interval=2e-4,
-              defer=True):
+              defer=True, raw=False):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
     ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
@@ -197,17 +231,34 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True
     (the drain thread needs the GIL around its engine call; at the default 5 ms it waits that long
     for the flows to yield, twice per drain); restored on return.  None leaves it alone.
     ``defer``: combines run in one batch at the end of the epoch (False: one engine call each,
-    when the instance asks; the reference's order, used to check the deferred path)."""
+    when the instance asks; the reference's order, used to check the deferred path).
+    ``raw``: the node receives bincode bytes (``trace.serialize()``): contributions are decoded in
+    one batch (DeserializeCiphertext faults, epoch_state.rs:377-381) and every window of share
+    messages in one batch before it is queued (hbbft_amd.wire)."""
     old = sys.getswitchinterval()
     if pipelined and switch_interval:
         sys.setswitchinterval(switch_interval)
     try:
-        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer)
+        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw)
     finally:
         sys.setswitchinterval(old)
 
 
-def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer):
+def _decoder(engine, raw_msgs, out, fn):
+    """decode(batch) for _deliver: fills out[(p, j)], returns the keys that did not decode."""
+    def decode(batch):
+        pts = fn(engine, [raw_msgs[m] for m in batch])
+        bad = set()
+        for m, pt in zip(batch, pts):
+            if pt is None:
+                bad.add(m)
+            else:
+                out[m] = pt
+        return bad
+    return decode
+
+
+def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     ver = BatchVerifier(engine)
@@ -238,22 +289,31 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
         if step.output:
             coin_out[p] = step.output[0]
     handed = {}  # (kind, proposer) -> senders handed to the instance, in order (for a replay)
+    coin_sh = {} if raw else trace.coin_shares
+    dec_sh = {} if raw else trace.dec_shares
 
     def hand_coin(p, j):
         handed.setdefault(("coin", p), []).append(j)
-        return ts[p].handle_message(j, trace.coin_shares[(p, j)])
+        return ts[p].handle_message(j, coin_sh[(p, j)])
 
     for p, out in _deliver(ver, trace.coin_msgs, window, ts,
-                           lambda p, j: ver.queue_sig(keys.pks[j], ts[p].doc_hash, trace.coin_shares[(p, j)]),
-                           hand_coin, res, "coin", pipelined, limit):
+                           lambda p, j: ver.queue_sig(keys.pks[j], ts[p].doc_hash, coin_sh[(p, j)]),
+                           hand_coin, res, "coin", pipelined, limit,
+                           _decoder(engine, trace.raw_coin, coin_sh, wire.decode_sig_share_msgs) if raw else None):
         coin_out[p] = out
     res.timing["coin_verify"] = time.perf_counter() - t0
 
     # --- Subset output: the N ciphertexts into ThresholdDecrypt
     t0 = time.perf_counter()
     ps = sorted(trace.cts)
-    huv = hoststage.hash_g1_g2([trace.cts[p][0] for p in ps], [trace.cts[p][1] for p in ps], threads=threads)
-    cts = {p: Ciphertext(trace.cts[p][0], trace.cts[p][1], trace.cts[p][2], h) for p, h in zip(ps, huv)}
+    if raw:  # the Subset outputs are serialised Ciphertexts: one batched decode
+        got = dict(zip(ps, wire.decode_ciphertexts(engine, [trace.raw_cts[p] for p in ps])))
+        res.faults += [("dec", p, Fault(p, "DeserializeCiphertext")) for p in ps if got[p] is None]
+        ps = [p for p in ps if got[p] is not None]
+    else:
+        got = trace.cts
+    huv = hoststage.hash_g1_g2([got[p][0] for p in ps], [got[p][1] for p in ps], threads=threads) if ps else []
+    cts = {p: Ciphertext(got[p][0], got[p][1], got[p][2], h) for p, h in zip(ps, huv)}
     own_dec = dict(zip(ps, hoststage.g1_mul([cts[p].u for p in ps], [sk] * len(ps), threads=threads)))
     by_u = {cts[p].u: own_dec[p] for p in ps}
     ni_dec = NetworkInfo(our, range(n), keys.t, keys.master_pk, keys.pks, decrypt_share=lambda U: by_u[bytes(U)])
@@ -264,8 +324,16 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     res.timing["decrypt_setup"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     dec_out = {}
-    for p in ps:
-        td[p].set_ciphertext(cts[p])
+    for p in list(ps):
+        try:
+            td[p].set_ciphertext(cts[p])
+        except ProtocolError as e:  # HoneyBadger faults the proposer (epoch_state.rs:388-391)
+            if e.kind != "InvalidCiphertext":
+                raise
+            res.faults.append(("dec", p, Fault(p, "InvalidCiphertext")))
+            del td[p]
+            ps.remove(p)
+            continue
         step = _input(td[p], "dec", p, res)
         res.faults += [("dec", p, f) for f in step.fault_log]
         if step.output:
@@ -273,11 +341,13 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
 
     def hand_dec(p, j):
         handed.setdefault(("dec", p), []).append(j)
-        return td[p].handle_message(j, trace.dec_shares[(p, j)])
+        return td[p].handle_message(j, dec_sh[(p, j)])
 
-    for p, out in _deliver(ver, trace.dec_msgs, window, td,
-                           lambda p, j: ver.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], cts[p].huv, cts[p].w),
-                           hand_dec, res, "dec", pipelined, limit):
+    dec_msgs = [m for m in trace.dec_msgs if m[0] in td]  # (shares of a faulted contribution: no instance)
+    for p, out in _deliver(ver, dec_msgs, window, td,
+                           lambda p, j: ver.queue_dec(keys.pks[j], dec_sh[(p, j)], cts[p].huv, cts[p].w),
+                           hand_dec, res, "dec", pipelined, limit,
+                           _decoder(engine, trace.raw_dec, dec_sh, wire.decode_dec_share_msgs) if raw else None):
         dec_out[p] = out
     res.timing["decrypt_verify"] = time.perf_counter() - t0
 
@@ -295,7 +365,7 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
             res.faults = [f for f in res.faults if f[:2] != (kind, p)]
             out = _replay(engine, kind, p, ni_sign if kind == "coin" else ni_dec,
                           ts[p].doc_hash if kind == "coin" else cts[p], handed.get((kind, p), []),
-                          trace.coin_shares if kind == "coin" else trace.dec_shares, res)
+                          coin_sh if kind == "coin" else dec_sh, res)
             if out is not None:
                 outs[p] = out
     sigs = {p: (d.result[0] if isinstance(d, Deferred) else d) for p, d in coin_out.items()}

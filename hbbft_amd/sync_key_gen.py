@@ -22,7 +22,7 @@ never leave the key generation, so only the node set has to agree on them.
 """
 import random
 
-from . import hoststage
+from . import hoststage, wire
 from ._lib import G1_BYTES
 
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
@@ -124,12 +124,20 @@ class Part:
     def __eq__(self, o):
         return isinstance(o, Part) and (self.degree, self.commit, self.rows) == (o.degree, o.commit, o.rows)
 
+    def to_bytes(self):
+        """bincode(Part) (hbbft_amd.wire)."""
+        return wire.encode_part(self.degree, self.commit, [(c.u, c.v, c.w) for c in self.rows])
+
 
 class Ack:
     """Ack(u64 proposer index, Vec<Ciphertext>) (sync_key_gen.rs:242)."""
 
     def __init__(self, proposer_idx, values):
         self.proposer_idx, self.values = proposer_idx, list(values)
+
+    def to_bytes(self):
+        """bincode(Ack) (hbbft_amd.wire)."""
+        return wire.encode_ack(self.proposer_idx, [(c.u, c.v, c.w) for c in self.values])
 
 
 class PartOutcome:
@@ -352,9 +360,28 @@ class SyncKeyGen:
                 outs[o].ack = Ack(sidx, cts[j * n:(j + 1) * n])
         return outs
 
+    def handle_part_msgs(self, items, rng=None):
+        """handle_parts over received bincode bytes: [(sender_id, bytes)].  The window's Parts are
+        decoded in one batch (hbbft_amd.wire: one GPU decompression for every commitment point and
+        ciphertext); a message that does not decode gets PartOutcome(fault="DeserializeMessage")
+        -- the reference's transport would drop it before handle_part -- and the others the
+        outcomes handle_parts gives them, in order."""
+        dec = wire.decode_parts(self.engine, [b for _, b in items])
+        good = [(sid, Part(d[0], d[1], [Ciphertext(*c) for c in d[2]])) for (sid, _), d in zip(items, dec)
+                if d is not None]
+        outs = iter(self.handle_parts(good, rng))
+        return [next(outs) if d is not None else PartOutcome(fault="DeserializeMessage") for d in dec]
+
     # -------------------------------------------------------------- Ack (sync_key_gen.rs:398-404, 515-547)
     def handle_ack(self, sender_id, ack):
         return self.handle_acks([(sender_id, ack)])[0]
+
+    def handle_ack_msgs(self, items):
+        """handle_acks over received bincode bytes (see handle_part_msgs)."""
+        dec = wire.decode_acks(self.engine, [b for _, b in items])
+        good = [(sid, Ack(d[0], [Ciphertext(*c) for c in d[1]])) for (sid, _), d in zip(items, dec) if d is not None]
+        outs = iter(self.handle_acks(good))
+        return [next(outs) if d is not None else AckOutcome(fault="DeserializeMessage") for d in dec]
 
     def handle_acks(self, items):
         n = len(self.pub_keys)
