@@ -42,10 +42,8 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
-IMPLS = {"lane_coop": 1, "thread_signed": 2, "auto": 3, "pair": 4, "wave": 5}   # HBH_IMPL_* (include/hbbft_hip.h)
-KERNEL_NAMES = {"lane_coop": "hbs::k_lc_* (miller+easy+exp+glue+verdict)",
-                "thread_signed": "hbs::k_ts_* (miller+easy+exp+glue+verdict)",
-                "pair": "hbs::k_pair_verify<false, true, 2>",
+IMPLS = {"auto": 3, "pair": 4, "wave": 5}   # HBH_IMPL_* (include/hbbft_hip.h)
+KERNEL_NAMES = {"pair": "hbs::k_pair_verify<false, true, 2>",
                 "wave": "hbs::k_wave (one wave per check)",
                 "auto": "hbs::k_pair_verify<false, true, 2>"}
 G1_UNC = bytes.fromhex(
@@ -398,7 +396,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
-    ap.add_argument("--impl", choices=["lane_coop", "thread_signed", "pair", "wave", "auto"], default="auto",
+    ap.add_argument("--impl", choices=["pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
     ap.add_argument("--no-pipeline", action="store_true",

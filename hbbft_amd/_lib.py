@@ -76,7 +76,7 @@ SIGNATURES = [
     ("hbh_encrypt", _I, [_SZ, _P, _I, _P, _P, _P, _P, _P, _P, _I]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
-IMPL_LANE_COOP, IMPL_THREAD_SIGNED, IMPL_AUTO, IMPL_PAIR, IMPL_WAVE = 1, 2, 3, 4, 5   # HBH_IMPL_* (0 = retired THREAD)
+IMPL_AUTO, IMPL_PAIR, IMPL_WAVE = 3, 4, 5   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)
 
 _lib = None
 

@@ -14,7 +14,6 @@
 #include "../../include/hbbft_hip.h"
 #include "launch.hpp"
 #include "interp_pair.hpp"
-#include "lcprep.hpp"
 #include "wire.hpp"
 
 namespace {
@@ -105,16 +104,13 @@ struct hbh_engine {
   std::vector<uint64_t> h_digits;
   std::vector<int> h_status;
   // workspaces
-  DevBuf coef1, coef2, inf1, inf2, work, status, lc0, lc1, lc2, lc3, g1rep, fbtab, ipart;
+  DevBuf work, status, fbtab, ipart;
   bool fbtab_ready = false;  // fixed-base comb table of g1 (built on first use)
-  size_t g1rep_n = 0;
   // staging for host-pointer entry points
   DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
 };
 
 namespace {
-
-using hbl::line_table_bytes;
 
 // Start of a call on stream s: order it after the engine's previous call.
 int begin_call(hbh_engine* e, hipStream_t s) {
@@ -130,35 +126,9 @@ int end_call(hbh_engine* e, hipStream_t s) {
   return HBH_OK;
 }
 
-// n copies of the G1 generator on the device, for the implementations that read P per check
-int g1_repeated(hbh_engine* e, hipStream_t s, size_t n, const void** out);
-
-// Line tables for up to two G2 point sets, in one launch.
-int launch_prepare(hbh_engine* e, hipStream_t s, const void* d_pts0, size_t n0, DevBuf& coef0, DevBuf& inf0,
-                   const void* d_pts1 = nullptr, size_t n1 = 0, DevBuf* coef1 = nullptr, DevBuf* inf1 = nullptr) {
-  if (n0 + n1 == 0) return HBH_OK;
-  if (n0) {
-    HBH_CHECK(coef0.ensure(line_table_bytes(n0)));
-    HBH_CHECK(inf0.ensure(n0));
-  }
-  if (n1) {
-    HBH_CHECK(coef1->ensure(line_table_bytes(n1)));
-    HBH_CHECK(inf1->ensure(n1));
-  }
-  hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
-  HBH_CHECK(hbl::lc_prep_pair(s, (int)n0, d_pts0, coef0.p, (uint8_t*)inf0.p, (int)n1, d_pts1, n1 ? coef1->p : nullptr,
-                              n1 ? (uint8_t*)inf1->p : nullptr));
-  e->timer.end(s, t);
-  return HBH_OK;
-}
-
 int resolve_impl(const hbh_engine* e, size_t n) {
   if (e->impl != HBH_IMPL_AUTO) return e->impl;
-  if (n <= HBH_AUTO_WAVE_MAX) return HBH_IMPL_WAVE;
-  return n < HBH_AUTO_LANE_COOP_MAX ? HBH_IMPL_LANE_COOP : HBH_IMPL_PAIR;
-}
-// PAIR and WAVE share the pair_prep line tables and the two table slots of the _dev calls
-bool uses_pair_tables(int impl) { return impl == HBH_IMPL_PAIR || impl == HBH_IMPL_WAVE;
+  return n <= HBH_AUTO_WAVE_MAX ? HBH_IMPL_WAVE : HBH_IMPL_PAIR;
 }
 
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
@@ -189,28 +159,6 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
   return HBH_OK;
 }
 
-// multi-Miller loop + final exponentiation over prepared tables (coef1/2, inf1/2)
-int launch_prepared(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_p1, size_t nq1,
-                    const uint32_t* d_i1, const void* d_p2, size_t nq2, const uint32_t* d_i2, int flags, uint8_t* d_v,
-                    uint32_t* d_value) {
-  hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  if (impl == HBH_IMPL_THREAD_SIGNED) {
-    const size_t bytes = hbl::ts_state_bytes((int)n);
-    for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
-    HBH_CHECK(hbl::ts_miller(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2, e->coef2.p,
-                             (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, e->lc0.p));
-    HBH_CHECK(hbl::ts_final_exp(s, (int)n, e->lc0.p, e->lc1.p, e->lc2.p, e->lc3.p, d_v, d_value));
-  } else {
-    const size_t bytes = hbl::lc_state_words((int)n) * sizeof(int32_t);
-    for (DevBuf* b : {&e->lc0, &e->lc1, &e->lc2, &e->lc3}) HBH_CHECK(b->ensure(bytes));
-    HBH_CHECK(hbl::lc_pairing(s, (int)n, d_p1, e->coef1.p, (int)nq1, (const uint8_t*)e->inf1.p, d_i1, d_p2,
-                              e->coef2.p, (int)nq2, (const uint8_t*)e->inf2.p, d_i2, flags, (int32_t*)e->lc0.p,
-                              (int32_t*)e->lc1.p, (int32_t*)e->lc2.p, (int32_t*)e->lc3.p, d_v, d_value));
-  }
-  e->timer.end(s, t);
-  return HBH_OK;
-}
-
 // e(P1_i, Q1[i1_i]) == e(P2_i, Q2[i2_i]) for device-resident inputs; d_p1 / d_p2 == nullptr means
 // the G1 generator for every check.  flags as hbl::pair_verify.
 int run_pairing_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
@@ -218,19 +166,8 @@ int run_pairing_dev(hbh_engine* e, hipStream_t s, size_t n, const void* d_p1, co
                     int flags, uint8_t* d_v, uint32_t* d_value = nullptr, int slot = 0) {
   if (n == 0) return HBH_OK;
   if (n > (size_t)1 << 30 || nq1 > (size_t)1 << 30 || nq2 > (size_t)1 << 30) return fail(HBH_ERR_ARG, "batch too large");
-  const int impl = resolve_impl(e, n);
-  if (uses_pair_tables(impl))
-    return launch_pair(e, s, impl, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value, slot);
-  if (!d_p1 || !d_p2) {
-    const void* g = nullptr;
-    int rc = g1_repeated(e, s, n, &g);
-    if (rc) return rc;
-    if (!d_p1) d_p1 = g;
-    if (!d_p2) d_p2 = g;
-  }
-  int rc = launch_prepare(e, s, d_q1, nq1, e->coef1, e->inf1, d_q2, nq2, &e->coef2, &e->inf2);
-  if (rc) return rc;
-  return launch_prepared(e, s, impl, n, d_p1, nq1, d_i1, d_p2, nq2, d_i2, flags, d_v, d_value);
+  return launch_pair(e, s, resolve_impl(e, n), n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, flags, d_v, d_value,
+                     slot);
 }
 
 int check_idx(const uint32_t* idx, size_t n, size_t table) {
@@ -281,27 +218,6 @@ int run_pairing_eq_host(hbh_engine* e, size_t n, const uint8_t* p1, const uint8_
   rc = end_call(e, s);
   if (rc) return rc;
   HBH_CHECK(hipStreamSynchronize(s));
-  return HBH_OK;
-}
-
-// G1 generator in the ABI format (canonical little-endian x || y).
-const uint32_t G1_GEN_WORDS[24] = {
-    0xdb22c6bbu, 0xfb3af00au, 0xf97a1aefu, 0x6c55e83fu, 0x171bac58u, 0xa14e3a3fu, 0x9774b905u, 0xc3688c4fu,
-    0x4fa9ac0fu, 0x2695638cu, 0x3197d794u, 0x17f1d3a7u, 0x46c5e7e1u, 0x0caa2329u, 0xa2888ae4u, 0xd03cc744u,
-    0x2c04b3edu, 0x00db18cbu, 0xd5d00af6u, 0xfcf5e095u, 0x741d8ae4u, 0xa09e30edu, 0xe3aaa0f1u, 0x08b3f481u};
-
-int g1_repeated(hbh_engine* e, hipStream_t s, size_t n, const void** out) {
-  if (e->g1rep_n < n) {
-    // grown rarely: the device copy persists for the engine's lifetime
-    const size_t want = n + n / 2 + 64;
-    std::vector<uint32_t> h(want * 24);
-    for (size_t i = 0; i < want; i++) std::memcpy(h.data() + i * 24, G1_GEN_WORDS, sizeof(G1_GEN_WORDS));
-    HBH_CHECK(e->g1rep.ensure(want * HBH_G1_BYTES));
-    HBH_CHECK(hipMemcpyAsync(e->g1rep.p, h.data(), want * HBH_G1_BYTES, hipMemcpyHostToDevice, s));
-    HBH_CHECK(hipStreamSynchronize(s));
-    e->g1rep_n = want;
-  }
-  *out = e->g1rep.p;
   return HBH_OK;
 }
 
@@ -359,8 +275,7 @@ int hbh_engine_destroy(hbh_engine* e) {
     if (ev) (void)hipEventSynchronize(ev);
   (void)hipStreamSynchronize(e->stream);
   e->timer.clear();
-  for (DevBuf* b : {&e->coef1, &e->coef2, &e->inf1, &e->inf2, &e->work, &e->status, &e->lc0, &e->lc1, &e->lc2, &e->lc3,
-                    &e->g1rep, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
+  for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
                     &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1]})
     b->release();
@@ -391,22 +306,16 @@ int hbh_verify_pairing_eq_dev(hbh_engine* e, void* stream, size_t n, const void*
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  if (n && uses_pair_tables(resolve_impl(e, n))) {
-    // table slot of its own: wait for the last general call and for this slot's previous user only
-    const int slot = e->slot;
-    e->slot ^= 1;
-    HBH_CHECK(hipStreamWaitEvent(s, e->done, 0));
-    HBH_CHECK(hipStreamWaitEvent(s, e->slot_done[slot], 0));
-    int rc = run_pairing_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, 1, d_v, nullptr, slot);
-    if (rc) return rc;
-    HBH_CHECK(hipEventRecord(e->slot_done[slot], s));
-    return HBH_OK;
-  }
-  int rc = begin_call(e, s);
+  if (n == 0) return HBH_OK;
+  // table slot of its own: wait for the last general call and for this slot's previous user only
+  const int slot = e->slot;
+  e->slot ^= 1;
+  HBH_CHECK(hipStreamWaitEvent(s, e->done, 0));
+  HBH_CHECK(hipStreamWaitEvent(s, e->slot_done[slot], 0));
+  int rc = run_pairing_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, 1, d_v, nullptr, slot);
   if (rc) return rc;
-  rc = run_pairing_dev(e, s, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, 1, d_v);
-  if (rc) return rc;
-  return end_call(e, s);
+  HBH_CHECK(hipEventRecord(e->slot_done[slot], s));
+  return HBH_OK;
 }
 
 int hbh_verify_sig_shares(hbh_engine* e, size_t n, const uint8_t* pks, const uint8_t* sigs, const uint8_t* hashes,
@@ -466,8 +375,7 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
-  if (impl != HBH_IMPL_LANE_COOP && impl != HBH_IMPL_THREAD_SIGNED && impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO &&
-      impl != HBH_IMPL_WAVE)
+  if (impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO && impl != HBH_IMPL_WAVE)
     return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;

@@ -2,7 +2,8 @@
 //
 // verdict[i] = e(P1_i, Q1_i) == e(P2_i, Q2_i), computed as FE(f_{|x|,Q1}(P1) f_{|x|,Q2}(-P2)) == 1 with
 // one 2-pair multi-Miller loop and one final exponentiation per check -- SURVEY §8(d)'s unit of work,
-// the same formulas as k_ts_miller / k_ts_fe (pairing.hpp, stower.hpp) on the lane-pair tower of
+// pairing 0.14's Miller loop and final exponentiation (oracle/c/bls_cpu.c miller_loop /
+// final_exponentiation restate them) on the lane-pair tower of
 // pfp.hpp: TWO lanes per check, so a 65,536-check batch is 2,048 waves = two waves per SIMD.
 //
 // Each G2 side is one of
@@ -90,10 +91,10 @@ HP_D H12 h_exp_abs_x(const H12& base) {
 HP_D H12 h_exp_x(const H12& f) { return h12_conj(h_exp_abs_x<false>(f)); }
 HP_D H12 h_exp_xm1(const H12& f) { return h12_conj(h_exp_abs_x<true>(f)); }
 
-// e = f^(3 (p^12 - 1) / r), the chain of pairing.hpp final_exp_x3 reordered so that at most one
+// e = f^(3 (p^12 - 1) / r), pairing 0.14's hard-part chain (x3) reordered so that at most one
 // Fp12 has to outlive an exponentiation (it waits in the LDS stash):
 //   g = f^((p^6 - 1)(p^2 + 1));  a = (g^(x-1))^(x-1);  b = a^x frob1(a);
-//   w = frob2(b) conj(b) g^3;    e = (b^x)^x w   (= c g^3 of pairing.hpp)
+//   w = frob2(b) conj(b) g^3;    e = (b^x)^x w
 HP_D H12 h_final_exp(const H12& f, uint32_t* __restrict__ stash) {
   const H12 f1 = h12_mul(h12_conj(f), h12_inv(f));
   const H12 g = h12_mul(h12_frob2(f1), f1);

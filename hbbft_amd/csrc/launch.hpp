@@ -1,5 +1,5 @@
 // Host-side launchers of the HIP kernels.  Each kernel family lives in its own translation unit
-// (k_prepare.hip, k_pair.hip, k_lc.hip, k_ts_*.hip, k_curve.hip, k_wire.hip) so the Makefile
+// (k_pair.hip, k_wave.hip, k_curve.hip, k_g1quad.hip, k_interp_pair.hip, k_wire.hip) so the Makefile
 // compiles them in parallel; engine.hip owns the C ABI, device buffers and streams and calls only
 // these functions.
 #pragma once
@@ -11,37 +11,6 @@ namespace hbl {
 
 constexpr int HBL_DUPLICATE = 5;  // == HBH_ERR_DUPLICATE_ENTRY
 constexpr int HBL_BAD_INDEX = 1;  // == HBH_ERR_ARG
-constexpr int MILLER_STEPS = 68;
-constexpr int LINE_Q4 = 21;  // 16-byte chunks per line (3 Fp2 x 14 limbs)
-inline int pad64(size_t n) { return (int)((n + 63) / 64 * 64); }
-inline size_t line_table_bytes(size_t npts) { return (size_t)MILLER_STEPS * LINE_Q4 * pad64(npts) * 16; }
-
-// --------------------------------------------------------------- line tables (k_prepare.hip)
-// Miller-loop line tables of up to two G2 point sets (ABI G2 words) in one launch, in the layout of
-// the lane-cooperative and one-thread signed kernels.
-hipError_t g2_prepare(hipStream_t s, int n0, const void* pts0, void* coef0, uint8_t* inf0, int n1, const void* pts1,
-                      void* coef1, uint8_t* inf1);
-
-// --------------------------------------------------------------- lane-cooperative pairing (k_lc.hip)
-// verdict[i] = e(P1_i, Q1[idx1_i]) == e(P2_i, Q2[idx2_i]) from prepared line tables (or, with value_out, e(P1,Q1)^3 e(P2,Q2)^3 words when flags has
-// bit 2 set and P2 = O), six lanes per check; w0..w3 are scratch of lc_state_words(n) int32 each.
-size_t lc_lstride(int n);
-size_t lc_state_words(int n);
-hipError_t lc_pairing(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
-                      const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,
-                      const uint32_t* idx2, int flags, int32_t* w0, int32_t* w1, int32_t* w2, int32_t* w3,
-                      uint8_t* verdict, uint32_t* value_out);
-
-// --------------------------------------------------------------- signed thread pairing (k_ts_*.hip)
-// The same verdicts / values as lc_pairing, one thread per check on signed limbs.  w0..w3 are
-// scratch of ts_state_bytes(n) each (the Fp12 state handed between stage kernels).
-size_t ts_state_bytes(int n);
-hipError_t ts_miller(hipStream_t s, int n, const void* p1, const void* coef1, int nq1, const uint8_t* inf1,
-                     const uint32_t* idx1, const void* p2, const void* coef2, int nq2, const uint8_t* inf2,
-                     const uint32_t* idx2, int flags, void* w0);
-hipError_t ts_final_exp(hipStream_t s, int n, void* w0, void* w1, void* w2, void* w3, uint8_t* verdict,
-                        uint32_t* value_out);
-
 // --------------------------------------------------------------- lane-pair pairing (k_pair.hip)
 // One side of a pairing-equality check.  TABLE side: `lines`/`qinf` from pair_prep over the nq
 // shared G2 points, `idx` picks the table per check.  WALK side (lines == nullptr): `q` holds G2

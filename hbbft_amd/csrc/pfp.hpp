@@ -21,7 +21,8 @@
 //   h_mul(a, b): a normalised or lazy (|limb| <= 2^29), b normalised, |a|, |b| < 16p -> normalised,
 //                |out| < 1.25p + |a||b| 2^-392 bound (column sums < 2^62.1).
 //   h_sqr(a)   : a normalised, |a| < 16p -> normalised (fp_mul_l contract (M) on (a0+-a1, a0-a1)).
-//   Fp12 values between operations are reduced (|.| < 2p), as in stower.hpp whose formulas these are.
+//   Fp12 values between operations are reduced (|.| < 2p).  The tower formulas are pairing 0.14's
+//   (restated in oracle/c/bls_cpu.c: Karatsuba Fp6, complex Fp12 squaring, Granger-Scott squaring).
 #pragma once
 #include "sfp.hpp"
 #include "words.hpp"
@@ -159,14 +160,6 @@ HP_D Fp h_const(const uint32_t (&c0)[NL], const uint32_t (&c1)[NL]) {
 // pair-wide AND of a per-lane flag
 HP_D bool lp_both(bool v) { return (v ? 1 : 0) & dpp<DPP_SWAP>(v ? 1 : 0); }
 HP_D bool h_is_zero(const Fp& a) { return lp_both(fp_is_zero(a)); }
-// 1 / a in Fp2: (a0 - a1 u) / (a0^2 + a1^2); both lanes invert the same norm
-HP_D Fp h_inv(const Fp& a) {
-  const Fp s = fp_sqr(a);
-  const Fp n = fp_reduce(fp_add(s, dpp_fp<DPP_SWAP>(s)));
-  const Fp t = fp_inv(n);
-  return h_conj(fp_mul(a, t));
-}
-
 // 1 / a in Fp2 with a variable-time inverse of the (public) norm: both lanes invert the same norm.
 // a = 0 gives 0 (the binary Euclid loop would not terminate on a zero norm).
 HP_D Fp h_inv_vartime(const Fp& a) {
@@ -245,7 +238,7 @@ HP_D H6 h6_neg(const H6& a) { return {fp_neg(a.c0), fp_neg(a.c1), fp_neg(a.c2)};
 HP_D H6 h6_red(const H6& a) { return {fp_reduce(a.c0), fp_reduce(a.c1), fp_reduce(a.c2)}; }
 HP_D H6 h6_mul_v(const H6& a) { return {h_mul_xi(a.c2), a.c0, a.c1}; }
 
-// Karatsuba (stower.hpp f6_mul), inputs < 4p
+// Karatsuba, inputs < 4p
 HP_D H6 h6_mul(const H6& a, const H6& b) {
   const Fp v0 = h_mul(a.c0, b.c0);
   const Fp v1 = h_mul(a.c1, b.c1);
@@ -277,7 +270,10 @@ HP_D H6 h6_inv(const H6& a) {
   const Fp c1 = fp_reduce(fp_sub(h_mul_xi(h_sqr(a.c2)), h_mul(a.c0, a.c1)));
   const Fp c2 = fp_reduce(fp_sub(h_sqr(a.c1), h_mul(a.c0, a.c2)));
   const Fp t = fp_reduce(fp_add(h_mul(a.c0, c0), h_mul_xi(fp_add(h_mul(a.c2, c1), h_mul(a.c1, c2)))));
-  const Fp ti = fp_reduce(h_inv(t));
+  // the final exponentiation's one inversion: values are public (share checks), so the binary-GCD
+  // inverse (25 rounds of 31 divsteps) replaces Fermat's 380 squarings + ~190 products (A/B on one
+  // box: sign 23.4 -> 22.7 ms, decrypt 21.6 -> 20.8 ms per 65,536 checks, profiles/r03/ab_inv.txt)
+  const Fp ti = fp_reduce(h_inv_vartime(t));
   return {h_mul(c0, ti), h_mul(c1, ti), h_mul(c2, ti)};
 }
 
@@ -299,7 +295,7 @@ HP_D H12 h12_mul(const H12& a, const H12& b) {
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_add(b.c0, b.c1));
   return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
 }
-// complex squaring (stower.hpp f12_sqr)
+// complex squaring
 HP_D H12 h12_sqr(const H12& a) {
   const H6 t = h6_red(h6_mul(a.c0, a.c1));
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_red(h6_add(a.c0, h6_mul_v(a.c1))));
@@ -369,7 +365,7 @@ HP_D H12 h12_frob2(const H12& f) {
   return r;
 }
 
-// Granger-Scott cyclotomic squaring (stower.hpp f12_cyclo_sqr), input reduced, output reduced.
+// Granger-Scott cyclotomic squaring, input reduced, output reduced.
 // Each output 3 A -/+ 2 a is formed from the unnormalised squares and reduced in one carry pass
 // (fp_red_mk) instead of normalising A, the linear combination and the reduction separately.
 HP_D H12 h12_cyclo_sqr(const H12& f) {
@@ -401,8 +397,8 @@ HP_D bool h12_is_one(const H12& f) {
   return lp_both(ok);
 }
 
-// ---------------------------------------------------------------- G2 walk (pairing.hpp formulas)
-// T in Jacobian coordinates; lines scaled as in pairing.hpp (the Fp2 factors die in the final
+// ---------------------------------------------------------------- G2 walk (pairing 0.14's line formulas)
+// T in Jacobian coordinates; lines scaled as pairing 0.14 scales them (the Fp2 factors die in the final
 // exponentiation).  Each lane holds its components of T, Q and the line.
 struct HJac { Fp x, y, z; };
 struct HLine { Fp c0, c1, c4; };

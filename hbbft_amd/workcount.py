@@ -27,7 +27,14 @@ G2_WALK = NBITS * DBL_STEP + NADD * ADD_STEP
 
 MILLER_2PAIR = NBITS * (F12_SQR + 2 * (F12_MUL_014 + LINE_EVAL)) + NADD * 2 * (F12_MUL_014 + LINE_EVAL)
 
-FP_INV = 380 + bin(0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAA9).count("1") - 1
+# The final exponentiation's one Fp inversion (of a public norm) is T. Pornin's binary GCD
+# (words.hpp words_inv_vartime): 25 rounds of 31 divsteps on 64-bit approximations; per round the
+# 2x2 update of (a, b) (2 x 12 limbs x 2 MADs each) and of the Bezout pair (u, v) with its
+# Montgomery division by 2^31 (2 x (24 + 12) MADs) = 120 MADs -> 3,000 MADs = 10 Fp products.
+# (Round 2 priced Fermat's a^(p-2): 380 squarings + 190 products.)
+BINGCD_ROUNDS = (2 * 381 - 1 + 30) // 31
+BINGCD_MADS = BINGCD_ROUNDS * 120
+FP_INV = BINGCD_MADS // 300
 F2_INV = 2 + FP_INV + 2
 F6_INV = 3 * (F2S + F2M) + 3 * F2M + F2_INV + 3 * F2M
 F12_INV = 2 * F6_MUL + F6_INV + 2 * F6_MUL
@@ -53,7 +60,7 @@ if __name__ == "__main__":
 # ---------------------------------------------------------------------------- MAD pricing
 MAD_PER_FPMUL = 300
 MAD_PER_FPSQR = 222
-FP_INV_SQR = 380                      # square-and-multiply over p-2: 380 squarings
+FP_INV_SQR = 0                        # binary-GCD inverse: no Fp squarings (Fermat had 380)
 
 
 def mads(fpmul, fpsqr=0):

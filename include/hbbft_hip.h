@@ -144,8 +144,7 @@ int hbh_verify_ciphertexts(hbh_engine* eng, size_t n, const uint8_t* u, const ui
  * generator for every item (PublicKeyShare::verify_g2 has P2 = g1, Ciphertext::verify P1 = g1).
  * Calls on different streams are ordered by the engine (each call waits for the previous call's
  * device work before reusing the engine's workspaces).  Index arrays live in device memory and are
- * not inspected on the host: with HBH_IMPL_PAIR an index >= its table size yields verdict 0; the
- * LANE_COOP / THREAD_SIGNED implementations require in-range indices. */
+ * not inspected on the host: an index >= its table size yields verdict 0 (both implementations). */
 int hbh_verify_pairing_eq_dev(hbh_engine* eng, void* stream, size_t n,
                               const void* d_p1, const void* d_q1_table, size_t nq1, const uint32_t* d_q1_idx,
                               const void* d_p2, const void* d_q2_table, size_t nq2, const uint32_t* d_q2_idx,
@@ -267,29 +266,27 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
                 const uint8_t* nonces, uint8_t* u_out, uint8_t* v_out, uint8_t* w_out, int threads);
 
 /* ---------------------------------------------------------------- implementation selection
- * Pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks them):
+ * Pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks them
+ * against each other and the C oracle):
  *   HBH_IMPL_PAIR (k_pair.hip): TWO lanes per check, each lane holding one component of every Fp2
  *     value; the Miller loop walks per-check G2 points in registers and reads line tables only for
  *     G2 points shared through an index map; Miller loop and final exponentiation in one kernel.
  *     Throughput path.
- *   HBH_IMPL_LANE_COOP (k_lc.hip): six lanes per check, one Fp2 coefficient of the Fp12
- *     accumulator per lane; lowest latency for small batches.
- *   HBH_IMPL_THREAD_SIGNED (k_ts_*.hip): one thread per check, stage kernels (round-1 path, kept
- *     as a cross-check).
  *   HBH_IMPL_WAVE (k_wave.hip): one 64-lane wave per check; the check's Fp2 products run on 32 lane
  *     pairs side by side.  Latency path (one check: the master check of combine_and_verify_sig).
- *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, LANE_COOP below
- *     HBH_AUTO_LANE_COOP_MAX, PAIR from there on.
- * HBH_IMPL_THREAD (0, the round-1 unsigned one-thread kernel) is retired: selecting it returns
- * HBH_ERR_ARG. */
+ *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, PAIR above (the
+ *     measured crossover, profiles/r03/crossover_wave_pair.txt: 8,192 checks 11.6 vs 13.0 ms,
+ *     12,288 checks 17.2 vs 13.1 ms).
+ * Retired (selecting them returns HBH_ERR_ARG): HBH_IMPL_THREAD (0, round 1's one-thread kernel),
+ * HBH_IMPL_LANE_COOP (1, six lanes per check) and HBH_IMPL_THREAD_SIGNED (2, one thread per check
+ * on signed limbs) -- WAVE and PAIR cover every batch size faster. */
 #define HBH_IMPL_THREAD 0
 #define HBH_IMPL_LANE_COOP 1
 #define HBH_IMPL_THREAD_SIGNED 2
 #define HBH_IMPL_AUTO 3
 #define HBH_IMPL_PAIR 4
 #define HBH_IMPL_WAVE 5
-#define HBH_AUTO_WAVE_MAX 5120
-#define HBH_AUTO_LANE_COOP_MAX 16384
+#define HBH_AUTO_WAVE_MAX 8192
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 
 /* ---------------------------------------------------------------- profiling

@@ -2,7 +2,8 @@
 sample, against the C oracle (oracle/c/bls_cpu.c, the pairing 0.14 restatement):
 
 * configs[1]: 65,536 ThresholdSign share checks (N=64, f=21, 1,024 documents, 1/64 forged), AUTO
-  (the lane-pair kernel) and THREAD_SIGNED, verdicts equal to each other and to the construction;
+  (the lane-pair kernel) and WAVE (one wave per check), verdicts equal to each other and to the
+  construction;
   256 sampled verdicts recomputed by the C oracle; 1,024 combines + master verify.
 * configs[2]: 65,536 decryption-share checks over 1,024 ciphertexts + 1,024 G1 combines, each equal
   to U * msk (C oracle).
@@ -16,7 +17,7 @@ import pytest
 
 from oracle import bls12_381 as C
 from oracle import cbls, tc
-from hbbft_amd._lib import IMPL_AUTO, IMPL_THREAD_SIGNED
+from hbbft_amd._lib import IMPL_AUTO, IMPL_WAVE
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
 
 pytestmark = pytest.mark.gpu
@@ -53,7 +54,7 @@ def sign_batch(engine):
     return dict(coeffs=coeffs, sks=sks, pks=pks, mpk=mpk, hashes=hashes, sigs=sigs, expected=expected)
 
 
-@pytest.mark.parametrize("impl", [IMPL_AUTO, IMPL_THREAD_SIGNED], ids=["auto", "thread_signed"])
+@pytest.mark.parametrize("impl", [IMPL_AUTO, IMPL_WAVE], ids=["auto", "wave"])
 def test_config1_65536_sig_shares(engine, sign_batch, impl):
     b = sign_batch
     n = NDOCS * N
@@ -71,18 +72,19 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
 
 
 def test_config1_wave_at_auto_threshold(engine, sign_batch):
-    """The wave-per-check kernel on the largest batch AUTO gives it (HBH_AUTO_WAVE_MAX = 5,120
-    checks: 80 documents of configs[1]), walking both G2 sides: verdicts equal the construction."""
-    from hbbft_amd._lib import IMPL_WAVE
+    """Both kernels at the AUTO boundary (HBH_AUTO_WAVE_MAX = 8,192 checks: 128 documents of
+    configs[1]): WAVE walks both G2 sides, PAIR reads H's line table; verdicts equal the construction."""
     b = sign_batch
-    n = 5120
-    engine.set_pairing_impl(IMPL_WAVE)
-    try:
-        v = engine.verify_sig_shares([b["pks"][i % N] for i in range(n)], b["sigs"][:n], b["hashes"][:n // N],
-                                     [i // N for i in range(n)])
-    finally:
-        engine.set_pairing_impl(IMPL_AUTO)
-    assert v == b["expected"][:n]
+    n = 8192
+    from hbbft_amd._lib import IMPL_PAIR
+    for impl in (IMPL_WAVE, IMPL_PAIR, IMPL_AUTO):
+        engine.set_pairing_impl(impl)
+        try:
+            v = engine.verify_sig_shares([b["pks"][i % N] for i in range(n)], b["sigs"][:n], b["hashes"][:n // N],
+                                         [i // N for i in range(n)])
+        finally:
+            engine.set_pairing_impl(IMPL_AUTO)
+        assert v == b["expected"][:n], impl
 
 
 def test_config1_combines(engine, sign_batch):

@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[1, 2, 4, 5, 3], ids=["lane_coop", "thread_signed", "pair", "wave", "auto"])
+@pytest.fixture(params=[4, 5, 3], ids=["pair", "wave", "auto"])
 def eng(engine, request):
-    """All pairing implementations (HBH_IMPL_LANE_COOP, HBH_IMPL_THREAD_SIGNED, HBH_IMPL_PAIR,
-    HBH_IMPL_WAVE and the default HBH_IMPL_AUTO) must give identical results."""
+    """Both pairing implementations (HBH_IMPL_PAIR, HBH_IMPL_WAVE) and the default HBH_IMPL_AUTO
+    must give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine
     engine.set_pairing_impl(3)
@@ -158,8 +158,10 @@ def test_verify_signatures_public_key_verify(eng):
     assert list(got) == want == [1, 1, 0, 0, 1]
 
 
-def test_retired_thread_impl_rejected(engine):
-    """HBH_IMPL_THREAD (0) is retired from the product build: selecting it is an argument error."""
+@pytest.mark.parametrize("impl", [0, 1, 2], ids=["thread", "lane_coop", "thread_signed"])
+def test_retired_impls_rejected(engine, impl):
+    """HBH_IMPL_THREAD (0), HBH_IMPL_LANE_COOP (1) and HBH_IMPL_THREAD_SIGNED (2) are retired from
+    the product build: selecting one is an argument error."""
     from hbbft_amd._lib import HbhError
     with pytest.raises(HbhError):
-        engine.set_pairing_impl(0)
+        engine.set_pairing_impl(impl)
