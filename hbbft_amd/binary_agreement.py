@@ -1,0 +1,154 @@
+"""The coin path of Binary Agreement (src/binary_agreement/binary_agreement.rs) over the GPU verifier.
+
+BinaryAgreement needs threshold cryptography in one place: the common coin of every epoch with
+``epoch % 3 == 2`` is a ThresholdSign over ``bincode((session_id, epoch))`` whose signature parity
+is the coin value (:395-405, :437-448).  This mirror keeps the reference's epoch machinery around
+that coin -- the epoch counter, the per-epoch coin state, the incoming queue that holds messages of
+future epochs and replays them when the epoch advances (:245-266, :489-519), the ``AgreementEpoch``
+faults (too far in the future :250-251, a second coin share of one sender for one future epoch
+:100-105), the decision rule (:411-432) -- and runs every coin share check through the
+``BatchVerifier`` (hbbft_amd.protocol), i.e. batched on the GPU.
+
+Out of scope: the Synchronized Binary Value broadcast and the Conf round (BVal / Aux /
+Conf / Term vote counting).  Their outcome -- the aux values an epoch's SBV broadcast outputs, and the completion of its
+Conf round -- is handed in by the driver (``sbv_output``, ``conf_round_complete``) at the points where
+the reference's handle_sbvb_step (:301-324) and try_finish_conf_round (:469-480) act on it.
+"""
+from .honey_badger import coin_document
+from .protocol import Fault, ProtocolError, Step, ThresholdSign, signature_parity
+
+__all__ = ["BinaryAgreementCoin", "MAX_FUTURE_EPOCHS"]
+
+MAX_FUTURE_EPOCHS = 1000  # BinaryAgreement::new (binary_agreement.rs:214)
+
+
+class BinaryAgreementCoin:
+    """One BinaryAgreement instance's epochs and coins.
+
+    session: (hb_id, hb_epoch, proposer_idx) -- BaSessionId{subset_id: EpochId{hb_id, hb_epoch},
+    proposer_idx} (subset.rs:182-185).  Messages are ``(epoch, share)`` -- MessageContent::Coin
+    with its epoch; Step messages are ``("all", (epoch, share))``; faults of the coin's
+    ThresholdSign are wrapped as ``CoinFault:<kind>`` (Step::extend_with(.., FaultKind::CoinFault,
+    ..), :397-400)."""
+
+    def __init__(self, netinfo, verifier, session, max_future_epochs=MAX_FUTURE_EPOCHS):
+        self.netinfo, self.verifier = netinfo, verifier
+        self.session = tuple(session)
+        self.max_future_epochs = max_future_epochs
+        self.epoch = 0
+        self.decision = None
+        self.estimated = None
+        self.conf_values = None
+        self.incoming = {}   # epoch -> {sender: share}: the incoming_queue of future epochs
+        self.queued = 0      # messages that went through the future-epoch queue
+        self.coins = {}      # epoch -> coin value (threshold coins only)
+        self.coin_decided, self.coin_value, self.ts = self._coin_state()
+
+    # ------------------------------------------------------------ coin state (:437-448)
+    def coin_document(self, epoch=None):
+        hb_id, hb_epoch, proposer = self.session
+        return coin_document(hb_id, hb_epoch, proposer, self.epoch if epoch is None else epoch)
+
+    def _coin_state(self):
+        if self.epoch % 3 == 0:
+            return True, True, None
+        if self.epoch % 3 == 1:
+            return True, False, None
+        ts = ThresholdSign(self.netinfo, self.verifier)
+        try:
+            ts.set_document(self.coin_document())
+        except ProtocolError as e:  # Error::InvokeCoin
+            raise ProtocolError("InvokeCoin", e.kind)
+        return False, None, ts
+
+    # ------------------------------------------------------------ messages (:245-266)
+    def handle_message(self, sender, epoch, share):
+        if self.decision is not None or epoch < self.epoch:  # Coin messages can expire
+            return Step()
+        if epoch > self.epoch + self.max_future_epochs:
+            return Step.fault(sender, "AgreementEpoch")
+        if epoch > self.epoch:
+            q = self.incoming.setdefault(epoch, {})
+            if sender in q:  # ReceivedMessages::insert: a second Coin for this epoch
+                return Step.fault(sender, "AgreementEpoch")
+            q[sender] = bytes(share)
+            self.queued += 1
+            return Step()
+        return self._handle_coin(sender, share)
+
+    def _handle_coin(self, sender, share):  # :355-363
+        if self.coin_decided:
+            return Step()
+        try:
+            ts_step = self.ts.handle_message(sender, share)
+        except ProtocolError as e:  # Error::HandleThresholdSign
+            raise ProtocolError("HandleThresholdSign", e.kind)
+        return self._on_coin_step(ts_step)
+
+    def _on_coin_step(self, ts_step):  # :394-405
+        epoch = self.epoch
+        step = Step(fault_log=[Fault(f.node_id, "CoinFault:" + f.kind) for f in ts_step.fault_log],
+                    messages=[(target, (epoch, share)) for target, share in ts_step.messages])
+        if ts_step.output and not self.coin_decided:
+            self.coin_decided, self.coin_value = True, signature_parity(ts_step.output[0])
+            self.coins[epoch] = self.coin_value
+            step.extend(self.try_update_epoch())
+        return step
+
+    # ------------------------------------------------------------ SBV broadcast / Conf round outcomes
+    def sbv_output(self, values):
+        """The epoch's SBV broadcast output its aux values (handle_sbvb_step, :301-324): with a
+        decided coin (epochs 0 and 1 mod 3, or a threshold coin already combined from the others'
+        shares) they become the Conf values at once and the epoch may advance; otherwise the Conf
+        round starts (send_conf, :366-380, sets the Conf values)."""
+        if self.decision is not None or self.conf_values is not None:
+            return Step()
+        self.conf_values = frozenset(values)
+        return self.try_update_epoch() if self.coin_decided else Step()
+
+    def conf_round_complete(self):
+        """N - f Conf messages arrived (try_finish_conf_round, :469-480): the coin is invoked --
+        our share is signed and broadcast -- unless it already decided."""
+        if self.decision is not None or self.conf_values is None or self.coin_decided:
+            return Step()
+        try:
+            ts_step = self.ts.sign()
+        except ProtocolError as e:  # Error::InvokeCoin
+            raise ProtocolError("InvokeCoin", e.kind)
+        return self._on_coin_step(ts_step).extend(self.try_update_epoch())
+
+    def try_update_epoch(self):  # :411-432
+        if self.decision is not None or not self.coin_decided or self.conf_values is None:
+            return Step()
+        coin = self.coin_value
+        definite = next(iter(self.conf_values)) if len(self.conf_values) == 1 else None
+        if definite == coin:
+            return self.decide(coin)
+        return self.update_epoch(coin if definite is None else definite)
+
+    def decide(self, b):  # :450-466 (the Term message is BA's, not the coin's: not modelled)
+        if self.decision is not None:
+            return Step()
+        self.decision = b
+        return Step(output=[b])
+
+    def update_epoch(self, b):  # :489-519
+        self.conf_values = None
+        self.epoch += 1
+        self.coin_decided, self.coin_value, self.ts = self._coin_state()
+        self.estimated = b
+        step = Step()
+        replay = sorted(self.incoming.pop(self.epoch, {}).items())  # BTreeMap<sender, ..> order
+        if replay and not self.coin_decided:
+            # the replayed shares' checks in one drain (the reference verifies them one by one as
+            # handle_message_content reaches them; verdicts are pure, so the Steps are the same)
+            for sender, share in replay:
+                pk = self.netinfo.public_key_share(sender)
+                if pk is not None:
+                    self.verifier.queue_sig(pk, self.ts.doc_hash, share)
+            self.verifier.drain()
+        for sender, share in replay:
+            step.extend(self._handle_coin(sender, share))
+            if self.decision is not None:
+                return step
+        return step

@@ -33,7 +33,7 @@ from . import hoststage
 from . import wire
 from .protocol import BatchVerifier, Ciphertext, Deferred, Fault, NetworkInfo, ProtocolError, Step, \
     ThresholdDecrypt, ThresholdSign, signature_parity
-from .sync_key_gen import G1_GEN, R_ORDER
+from .sync_key_gen import G1_GEN, G2_GEN, R_ORDER
 
 __all__ = ["NetworkKeys", "EpochTrace", "coin_document", "run_epoch", "EpochResult"]
 
@@ -84,38 +84,80 @@ class EpochTrace:
 
     @classmethod
     def generate(cls, engine, keys, rng, hb_epoch=0, coins=None, proposal_bytes=256, bad_every=64, hb_id=0,
-                 our=0):
+                 our=0, n_adv=0, adversary="silent", inject=0.1):
+        """Node ``our``'s view of one epoch.  ``bad_every``: every bad_every-th share of an honest
+        sender is forged (None: none).  ``n_adv`` nodes (ids n - n_adv .. n - 1, as the reference's
+        TestNetwork numbers them) are adversarial: they propose nothing and send no correct share;
+        ``adversary`` says what they send instead (tests/honey_badger.rs):
+          "silent"       nothing (SilentAdversary);
+          "faulty_share" FaultyShareAdversary (:26-115): every adversarial node broadcasts, for
+                         every proposer, its (correct) decryption share of a FAKE ciphertext --
+                         encrypt(b"X marks the spot") to the master key;
+          "random"       RandomAdversary (:236-245, tests/network/mod.rs:237-350): about
+                         ``inject`` x (honest messages) messages injected from random adversarial
+                         senders, each a random coin (G2) or decryption (G1) share -- random valid
+                         subgroup points, rand::random()'s Message -- for a random instance."""
         n = keys.n
+        adv = set(range(n - n_adv, n))
+        assert our not in adv
+        good = [p for p in range(n) if p not in adv]
         coins = n if coins is None else coins
-        proposals = {p: bytes(rng.randrange(256) for _ in range(proposal_bytes)) for p in range(n)}
-        enc = hoststage.encrypt([keys.master_pk], [proposals[p] for p in range(n)],
-                                [rng.randrange(1, R_ORDER) for _ in range(n)])
-        cts = {p: enc[p] for p in range(n)}
+        proposals = {p: bytes(rng.randrange(256) for _ in range(proposal_bytes)) for p in good}
+        enc = hoststage.encrypt([keys.master_pk], [proposals[p] for p in good],
+                                [rng.randrange(1, R_ORDER) for _ in good])
+        cts = dict(zip(good, enc))
         coin_docs = {p: coin_document(hb_id, hb_epoch, p, 2) for p in rng.sample(range(n), coins)}
         hashes = dict(zip(coin_docs, hoststage.hash_g2([coin_docs[p] for p in coin_docs]))) if coins else {}
-        others = [j for j in range(n) if j != our]
+        others = [j for j in good if j != our]
         bad = set()
+
+        def forged(p, j, k):
+            return bad_every is not None and (p * n + j) % bad_every == k
+
         # decryption shares D_{p,j} = U_p * sk_j (a few forged: U_p * random)
         keys_d, bases, scal = [], [], []
-        for p in range(n):
+        for p in good:
             for j in others:
-                forged = (p * n + j) % bad_every == 1
+                fk = forged(p, j, 1)
                 keys_d.append((p, j))
                 bases.append(cts[p][0])
-                scal.append(rng.randrange(1, R_ORDER) if forged else keys.sks[j])
-                if forged:
+                scal.append(rng.randrange(1, R_ORDER) if fk else keys.sks[j])
+                if fk:
                     bad.add(("dec", p, j))
+        if adversary == "faulty_share" and adv:
+            fake_u = hoststage.encrypt([keys.master_pk], [b"X marks the spot"], [rng.randrange(1, R_ORDER)])[0][0]
+            for a in sorted(adv):
+                for p in good:  # (shares for proposers without a contribution reach no instance)
+                    keys_d.append((p, a))
+                    bases.append(fake_u)
+                    scal.append(keys.sks[a])
+                    bad.add(("dec", p, a))
         dec_shares = dict(zip(keys_d, engine.g1_mul(bases, scal))) if keys_d else {}
         keys_s, bases, scal = [], [], []
         for p in coin_docs:
             for j in others:
-                forged = (p * n + j) % bad_every == 2
+                fk = forged(p, j, 2)
                 keys_s.append((p, j))
                 bases.append(hashes[p])
-                scal.append(rng.randrange(1, R_ORDER) if forged else keys.sks[j])
-                if forged:
+                scal.append(rng.randrange(1, R_ORDER) if fk else keys.sks[j])
+                if fk:
                     bad.add(("coin", p, j))
         coin_shares = dict(zip(keys_s, engine.g2_mul(bases, scal))) if keys_s else {}
+        if adversary == "random" and adv:
+            slots = [("coin", p, a) for p in coin_docs for a in adv] + [("dec", p, a) for p in cts for a in adv]
+            k = min(len(slots), max(1, int(inject * (len(keys_d) + len(keys_s)))))
+            picks = rng.sample(slots, k)
+            g1_keys = [(p, a) for kind, p, a in picks if kind == "dec"]
+            g2_keys = [(p, a) for kind, p, a in picks if kind == "coin"]
+            if g1_keys:
+                dec_shares.update(zip(g1_keys, engine.g1_mul([G1_GEN] * len(g1_keys),
+                                                             [rng.randrange(1, R_ORDER) for _ in g1_keys])))
+            if g2_keys:
+                coin_shares.update(zip(g2_keys, engine.g2_mul([G2_GEN] * len(g2_keys),
+                                                              [rng.randrange(1, R_ORDER) for _ in g2_keys])))
+            keys_d += g1_keys
+            keys_s += g2_keys
+            bad.update(picks)
         coin_msgs = list(keys_s)
         rng.shuffle(coin_msgs)
         dec_msgs = list(keys_d)

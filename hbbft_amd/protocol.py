@@ -345,8 +345,8 @@ class BatchVerifier:
 
     def _run_jobs(self, jobs):
         """The engine calls of a snapshot (any thread): [(kind, keys, verdict bytes)]."""
-        fn = {"ct": self.eng.verify_ciphertexts, "sig": self.eng.verify_sig_shares, "dec": self.eng.verify_dec_shares}
-        return [(kind, keys, fn[kind](*args)) for kind, keys, args in jobs]
+        fn = {"ct": "verify_ciphertexts", "sig": "verify_sig_shares", "dec": "verify_dec_shares"}
+        return [(kind, keys, getattr(self.eng, fn[kind])(*args)) for kind, keys, args in jobs]
 
     def _store(self, results):
         """Cache verdicts (main thread) and return them as {(kind, instance, item): verdict}.

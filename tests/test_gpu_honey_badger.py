@@ -96,3 +96,68 @@ def test_failed_deferred_combine_is_replayed(engine):
                      sorted((k, p, f.node_id, f.kind) for k, p, f in r.faults))
     assert key(dfr) == key(imm)
     assert (imm.plaintexts, imm.coins) == (dfr.plaintexts, dfr.coins)
+
+
+def max_faulty(n):  # src/util.rs:22-25
+    return (n - 1) // 3
+
+
+@pytest.mark.parametrize("adversary", ["silent", "faulty_share", "random"])
+def test_epoch_adversaries_different_sizes(engine, adversary):
+    """tests/honey_badger.rs:191-245 through the GPU verifier: network sizes 1, 2, 3, 5 and one of
+    6..9 with max_faulty(size) adversarial nodes that propose nothing and send no correct share --
+    SilentAdversary, FaultyShareAdversary (every adversarial node broadcasts, for every proposer,
+    its decryption share of a fake ciphertext) and RandomAdversary (random coin / decryption shares
+    injected from adversarial senders).  Every contribution decrypts to its proposal, every coin is
+    msk * H with the oracle's parity, only adversarial senders are ever blamed, and the windowed
+    pipelined epoch equals per-message handling (window 1)."""
+    rng = random.Random({"silent": 71, "faulty_share": 72, "random": 73}[adversary])
+    sizes = [1, 2, 3, 5, rng.randrange(6, 10)]
+    blamed_total = 0
+    for size in sizes:
+        f = max_faulty(size)
+        keys = NetworkKeys(engine, size, f, rng)
+        trace = EpochTrace.generate(engine, keys, rng, hb_epoch=len(sizes), bad_every=None, proposal_bytes=40,
+                                    n_adv=f, adversary=adversary, inject=0.5)
+        res = run_epoch(engine, keys, trace, window=5)
+        check(trace, res, keys)
+        assert sorted(res.plaintexts) == list(range(size - f))
+        assert all(flt.node_id >= size - f for _, _, flt in res.faults), (size, res.faults)
+        assert res.errors == []
+        one = run_epoch(engine, keys, trace, window=1, pipelined=False)
+        assert (one.plaintexts, one.coins, one.signatures) == (res.plaintexts, res.coins, res.signatures)
+        assert sorted((k, p, x.node_id) for k, p, x in one.faults) == sorted((k, p, x.node_id) for k, p, x in res.faults)
+        blamed_total += len(res.faults)
+    if adversary == "silent":
+        assert blamed_total == 0
+    else:
+        assert blamed_total > 0
+
+
+def test_epoch_random_adversary_raw_bytes(engine):
+    """RandomAdversary on the wire (tests/honey_badger.rs:235-245): the node receives bincode bytes;
+    injected messages are random shares or bytes that do not decode (truncated, or a compressed x
+    off the curve).  Undecodable messages are DeserializeMessage faults of their (adversarial)
+    senders, decodable forged shares UnverifiedDecryptionShareSender / UnverifiedSignatureShareSender;
+    outputs equal the proposals and the oracle's coins."""
+    rng = random.Random(745)
+    n, f = 7, 2
+    keys = NetworkKeys(engine, n, f, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=3, bad_every=None, proposal_bytes=64, n_adv=f,
+                                adversary="random", inject=0.5)
+    injected = sorted(trace.bad)
+    garbage = injected[::3]
+    trace.serialize(corrupt=garbage)
+    res = run_epoch(engine, keys, trace, window=6, raw=True)
+    assert res.plaintexts == trace.proposals
+    for p, sig in res.signatures.items():
+        assert sig == cbls.g2_mul(trace.hashes[p], keys.msk)
+        assert res.coins[p] == parity_oracle(sig)
+    kinds = {"coin": "UnverifiedSignatureShareSender", "dec": "UnverifiedDecryptionShareSender"}
+    assert res.faults
+    for kind, p, flt in res.faults:
+        assert (kind, p, flt.node_id) in trace.bad and flt.node_id >= n - f
+        want = "DeserializeMessage" if (kind, p, flt.node_id) in garbage else kinds[kind]
+        assert flt.kind == want, (kind, p, flt)
+    # every undecodable message is blamed whether or not its instance is still running
+    assert {(k, p, x.node_id) for k, p, x in res.faults if x.kind == "DeserializeMessage"} == set(garbage)
