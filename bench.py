@@ -229,9 +229,10 @@ def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_sim
          "achieved": achieved, "peak": MAD_PEAK_MEASURED, "frac": achieved / MAD_PEAK_MEASURED,
          "peak_theoretical": MAD_PEAK_THEORETICAL, "traffic": pmc_traffic(kernel)}
     if waves_per_simd:
-        ceil = MAD_CEILING_BY_WAVES.get(waves_per_simd)
-        if ceil is None:  # below one wave per SIMD on average: the 1-wave ceiling scaled by occupancy
-            ceil = MAD_CEILING_BY_WAVES[1] * min(1.0, waves_per_simd)
+        if waves_per_simd < 1:  # below one wave per SIMD on average: the 1-wave ceiling scaled by occupancy
+            ceil = MAD_CEILING_BY_WAVES[1] * waves_per_simd
+        else:  # the measured ceiling of the largest measured occupancy not above it
+            ceil = MAD_CEILING_BY_WAVES[max(k for k in MAD_CEILING_BY_WAVES if k <= waves_per_simd)]
         e["waves_per_simd"] = waves_per_simd
         e["occupancy_ceiling"] = ceil
         e["frac_of_occupancy_ceiling"] = achieved / ceil
@@ -399,6 +400,9 @@ def main():
     ap.add_argument("--impl", choices=["pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
+    ap.add_argument("--dkg-scope", choices=["network", "node"], default="network",
+                    help="dkg workload: the whole network's 10^6 ack checks split over the ranks, or one node's "
+                         "10,000 per rank")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="epoch workload: drain each window before handling it (no GPU/host overlap)")
     ap.add_argument("--launcher", choices=["ranks", "pool"], default="ranks",
@@ -684,44 +688,62 @@ def cpu_baseline_decrypt(shares, pks, huv, ws, us, inst, expected, cidx, cpts, m
             "single_thread_value": n1 / st, "combine_g1_ms": comb_ms, "nproc": ncpu, "affinity": aff}
 
 
-def run_dkg(args, eng, world, rank, dev):
-    """configs[3]: SyncKeyGen N=100 t=33 -- the 10,000 Ack checks of one node
-    (BivarCommitment::evaluate == g1*val, src/sync_key_gen.rs:542) over 100 Parts with 595-point
-    commitments; ranks split the checks by Part (weak scaling: every rank plays one node)."""
-    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
-    rng = random.Random(100 + rank)
-    n_nodes, t = 100, 33
+def dkg_workload(eng, seed, n_nodes, t, nodes, tamper_every=97):
+    """SyncKeyGen acks of configs[3]: n_nodes random degree-t bivariate polynomials (the Parts) and,
+    for every checking node x in ``nodes`` (1-based), the acks (proposer p, sender y) of all
+    n_nodes x n_nodes pairs with val = f_p(x, y) -- every value a node decrypts from an Ack
+    (src/sync_key_gen.rs:515-547) -- 1/tamper_every of them tampered.  Values come from one
+    object-array matrix product per Part (rows = X C, vals = rows Y^T mod r).
+    Returns (commits, pidx, xs, ys, vals as n x 32 uint8 LE, expected verdict bytes)."""
+    rng = random.Random(seed)
     npos = (t + 1) * (t + 2) // 2
-    g1 = g1a(G1_UNC)
-    parts = []
-    coefs = []
-    for _ in range(n_nodes):
-        c = [rng.randrange(1, R_ORDER) for _ in range(npos)]
-        coefs.append(c)
-    flat = eng.g1_mul([g1] * (n_nodes * npos), [x for c in coefs for x in c])
-    parts = [flat[p * npos:(p + 1) * npos] for p in range(n_nodes)]
-    x = rank + 1
-    pidx, xs, ys, vals = [], [], [], []
 
     def cp(i, j):
         return j * (j + 1) // 2 + i if i <= j else i * (i + 1) // 2 + j
 
+    coefs = [[rng.randrange(1, R_ORDER) for _ in range(npos)] for _ in range(n_nodes)]
+    commits = eng.g1_mul_gen([c for cs in coefs for c in cs])
+    commits = [commits[p * npos:(p + 1) * npos] for p in range(n_nodes)]
+    nodes = list(nodes)
+    X = np.array([[pow(x, i) for i in range(t + 1)] for x in nodes], dtype=object)
+    Y = np.array([[pow(y, j) for y in range(1, n_nodes + 1)] for j in range(t + 1)], dtype=object)
+    vals = []   # per node x, per part p: n_nodes values
     for p in range(n_nodes):
-        xp = [pow(x, i, R_ORDER) for i in range(t + 1)]
-        row = [sum(coefs[p][cp(i, j)] * xp[i] for i in range(t + 1)) % R_ORDER for j in range(t + 1)]
-        for y in range(1, n_nodes + 1):
-            v = 0
-            for j in reversed(range(t + 1)):
-                v = (v * y + row[j]) % R_ORDER
-            pidx.append(p)
-            xs.append(x)
-            ys.append(y)
-            vals.append(v)
-    bad = set(range(0, len(vals), 97))
+        C = np.array([[coefs[p][cp(i, j)] for j in range(t + 1)] for i in range(t + 1)], dtype=object)
+        vals.append(((X @ C) % R_ORDER) @ Y % R_ORDER)     # [x][y]
+    nx, n = len(nodes), len(nodes) * n_nodes * n_nodes
+    pidx = np.repeat(np.tile(np.arange(n_nodes, dtype=np.uint32), nx), n_nodes)
+    xs = np.repeat(np.array(nodes, dtype=np.uint32), n_nodes * n_nodes)
+    ys = np.tile(np.arange(1, n_nodes + 1, dtype=np.uint32), nx * n_nodes)
+    flat = [int(vals[p][k][y]) for k in range(nx) for p in range(n_nodes) for y in range(n_nodes)]
+    bad = set(range(0, n, tamper_every))
     for a in bad:
-        vals[a] = (vals[a] + 1) % R_ORDER
-    expected = bytes(0 if a in bad else 1 for a in range(len(vals)))
-    v = eng.bivar_ack_check(t, parts, pidx, xs, ys, vals)
+        flat[a] = (flat[a] + 1) % R_ORDER
+    vb = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in flat), dtype=np.uint8).reshape(n, 32)
+    expected = bytes(0 if a in bad else 1 for a in range(n))
+    return commits, pidx, xs, ys, vb, expected
+
+
+def run_dkg(args, eng, world, rank, dev):
+    """configs[3]: SyncKeyGen N=100 t=33 Ack checks (BivarCommitment::evaluate == g1*val,
+    src/sync_key_gen.rs:542) over 100 Parts with 595-point commitments, held in a device-resident
+    commitment set (uploaded once, as a SyncKeyGen instance keeps them).
+    --dkg-scope network (default): the whole network's 10^6 checks -- all 100 nodes' 10,000 acks --
+      split by checking node over the ranks (strong scaling: the total is fixed);
+    --dkg-scope node: one node's 10,000 acks per rank (weak scaling: every rank plays one node)."""
+    n_nodes, t = 100, 33
+    npos = (t + 1) * (t + 2) // 2
+    network = args.dkg_scope == "network"
+    if network:
+        nodes = [x for x in range(1, n_nodes + 1) if (x - 1) % world == rank]
+    else:
+        nodes = [rank + 1]
+    t0 = time.perf_counter()
+    commits, pidx, xs, ys, vals, expected = dkg_workload(eng, 100, n_nodes, t, nodes)
+    gen_s = time.perf_counter() - t0
+    cs = eng.commit_set(t)
+    cs.add(commits)
+    v = cs.ack_check(pidx, xs, ys, vals)            # warm-up: builds the rows row(x) once
     ok = v == expected
     if world > 1:
         dist.barrier()
@@ -732,52 +754,69 @@ def run_dkg(args, eng, world, rank, dev):
     eng.set_profiling(True)
     for _ in range(nsteps):
         t0 = time.perf_counter()
-        v = eng.bivar_ack_check(t, parts, pidx, xs, ys, vals)
+        v = cs.ack_check(pidx, xs, ys, vals)
         times.append((time.perf_counter() - t0) * 1e3)
         ok = ok and v == expected
     dev_ms, dev_n = eng.stage_time(STAGE_CURVE)
     eng.set_profiling(False)
     dev_ms /= max(dev_n, 1)
+    nack = len(vals)
+    # row build (once per (part, x), cached in the set) timed separately on a fresh set
+    cs2 = eng.commit_set(t)
+    cs2.add(commits)
+    eng.set_profiling(True)
+    cs2.ack_check(pidx[:1], xs[:1], ys[:1], vals[:1])
+    row_ms, _ = eng.stage_time(STAGE_CURVE)
+    eng.set_profiling(False)
+    cs2.close()
     ms = _max_over_ranks(dev_ms, world, dev)
     host_ms = _max_over_ranks(statistics.median(times), world, dev)
-    per_rank = gather_per_rank({"rank": rank, "device_ms": dev_ms, "host_ms": statistics.median(times), "ok": ok},
-                               world)
+    per_rank = gather_per_rank({"rank": rank, "device_ms": dev_ms, "host_ms": statistics.median(times), "ok": ok,
+                                "acks": nack, "nodes": len(nodes)}, world)
     ok = all(r["ok"] for r in per_rank)
+    total = sum(r["acks"] for r in per_rank)
     if rank == 0:
-        nack = len(vals)
-        ops = [workcount.bivar_ack(t, y) for y in ys]
-        op = (sum(o[0] for o in ops) / nack, sum(o[1] for o in ops) / nack)
-        main_k = roofline_entry("hb::k_bivar_row + hbs::k_bivar_check_quad", dev_n, dev_ms, nack, op, "ack check",
-                                4 * nack / 64 / 1024)
+        ops = [workcount.bivar_ack(t, y) for y in range(1, n_nodes + 1)]
+        op = (sum(o[0] for o in ops) / n_nodes, sum(o[1] for o in ops) / n_nodes)
+        waves = 4 * nack / 64 / 1024
+        main_k = roofline_entry("hbs::k_bivar_check_quad", dev_n, dev_ms, nack, op, "ack check", waves)
         line = {
-            "metric": "SyncKeyGen ack checks/sec (whole node set), N=100 t=33", "value": nack * world / (ms / 1e3),
-            "unit": "acks/s", "n_gpus": world, "steps": nsteps, "warmup": 1, "ms_per_step": ms,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
+            "metric": "SyncKeyGen ack checks/sec (%s), N=100 t=33" % ("whole network" if network else "whole node set"),
+            "value": total / (ms / 1e3), "unit": "acks/s", "n_gpus": world, "steps": nsteps, "warmup": 1,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if network else "weak",
+            "vs_baseline": None, "dtype": "u32 limbs (Fp, 14x28-bit)",
             "data": "synthetic, seeded (100 random degree-33 bivariate polynomials; 1/97 tampered values)",
-            "config": {"workload": "SyncKeyGen ack checks of one node, BASELINE configs[3]", "acks_per_rank": nack,
-                       "parts": n_nodes, "commitment_points": npos, "parallelism": "one node per rank x%d" % world,
-                       "timing": "device time of the row + check kernels (HIP events); host_to_host_ms includes "
-                                 "the 5.7 MB commitment upload"},
-            "host_to_host_ms": host_ms, "verdicts_ok": ok, "per_rank": per_rank,
+            "config": {"workload": "SyncKeyGen ack checks, BASELINE configs[3]", "scope": args.dkg_scope,
+                       "total_acks": total, "acks_per_rank": nack, "checking_nodes_per_rank": len(nodes),
+                       "parts": n_nodes, "commitment_points": npos,
+                       "parallelism": ("checking nodes split over %d ranks" if network else "one node per rank x%d")
+                       % world,
+                       "timing": "device time of the ack-check kernel (HIP events) with the commitments and rows "
+                                 "resident in HBM (commitment set); host_to_host_ms: the whole call incl. the "
+                                 "upload of indices and values"},
+            "host_to_host_ms": host_ms, "row_build_ms": row_ms, "rows": len(nodes) * n_nodes,
+            "data_gen_s": round(gen_s, 2), "verdicts_ok": ok, "per_rank": per_rank,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
                              traffic=pmc_traffic("hbs::k_bivar_check_quad"),
-                             note="four lanes per ack (lane quads), 10,000 acks = 625 waves: latency-bound at "
-                                  "this size (0.6 waves per SIMD)"),
+                             note="four lanes per ack (lane quads); %.1f waves per SIMD" % waves),
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, g1)
+            line["cpu_baseline"] = cpu_baseline_dkg(t, commits, pidx, xs, ys, vals, expected, eng)
         print(json.dumps(line), flush=True)
+    cs.close()
 
 
-def cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, g1, per_thread=16):
+def cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, eng, per_thread=16):
     """The reference's ack check (BivarCommitment::evaluate(x, y) == g1 * val, sync_key_gen.rs:542,
     C restatement: 595-term evaluation + one scalar multiplication) on a bounded sample."""
+    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
     cbls = _ensure_oracle()
     ncpu, aff, threads = cpu_info()
+    g1 = g1a(G1_UNC)
 
     def check(a):
-        lhs = cbls.bivar_evaluate(t, parts[pidx[a]], xs[a], ys[a])
-        return lhs == cbls.g1_mul(g1, vals[a])
+        lhs = cbls.bivar_evaluate(t, parts[int(pidx[a])], int(xs[a]), int(ys[a]))
+        return lhs == cbls.g1_mul(g1, int.from_bytes(bytes(vals[a]), "little"))
 
     n1 = 8
     st, v = timed_pool(check, list(range(n1)), 1)

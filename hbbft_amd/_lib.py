@@ -41,6 +41,12 @@ SIGNATURES = [
     ("hbh_g2_decompress", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_commitment_eval", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P]),
     ("hbh_bivar_ack_check", _I, [_P, _SZ, _I, _SZ, _P, _P, _P, _P, _P, _P]),
+    ("hbh_commit_set_create", _I, [_P, _I, _c.POINTER(_P)]),
+    ("hbh_commit_set_destroy", _I, [_P]),
+    ("hbh_commit_set_add", _I, [_P, _SZ, _P, _c.POINTER(_SZ)]),
+    ("hbh_commit_set_size", _I, [_P, _c.POINTER(_SZ), _c.POINTER(_SZ)]),
+    ("hbh_bivar_row_set", _I, [_P, _SZ, _P, _P, _P]),
+    ("hbh_bivar_ack_check_set", _I, [_P, _SZ, _P, _P, _P, _P, _P]),
     ("hbh_engine_set_pairing_impl", _I, [_P, _I]),
     ("hbh_engine_set_profiling", _I, [_P, _I]),
     ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),

@@ -1170,3 +1170,237 @@ int hbh_g1_mul_gen(hbh_engine* e, size_t n, const uint8_t* scalars, uint8_t* out
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- device-resident commitment sets
+// ProposalState::commit (src/sync_key_gen.rs:254-262) lives as long as the SyncKeyGen instance and
+// is read by every row check (:496) and every Ack check (:542): a set keeps such commitments in HBM
+// (uploaded once) together with the Jacobian rows row(x) computed so far, so an Ack drain uploads
+// only its indices and values.
+struct hbh_commit_set {
+  hbh_engine* e = nullptr;
+  int t = 0;
+  size_t ncoef = 0;
+  size_t nparts = 0;
+  void* commits = nullptr;  // nparts * ncoef ABI G1 points
+  size_t commits_cap = 0;   // bytes
+  std::unordered_map<uint64_t, uint32_t> row_slot;  // (part << 32 | x) -> row
+  size_t nrows = 0;
+  void* rows = nullptr;     // nrows Jacobian rows (hbl::bivar_rows_quad_bytes(1, t) each)
+  size_t rows_cap = 0;      // bytes
+  DevBuf stage;             // indices of rows computed by a call
+};
+
+namespace {
+// Grow a device allocation to at least `want` bytes, keeping its first `used` bytes.
+int grow_keep(hipStream_t s, void** p, size_t* cap, size_t used, size_t want) {
+  if (want <= *cap) return HBH_OK;
+  const size_t nc = std::max(want, *cap * 2);
+  void* q = nullptr;
+  HBH_CHECK(hipMalloc(&q, nc));
+  if (used) HBH_CHECK(hipMemcpyAsync(q, *p, used, hipMemcpyDeviceToDevice, s));
+  HBH_CHECK(hipStreamSynchronize(s));
+  if (*p) HBH_CHECK(hipFree(*p));
+  *p = q;
+  *cap = nc;
+  return HBH_OK;
+}
+
+// Row slots for n (part, x) requests; rows not cached yet are computed on stream s (k_bivar_row_quad
+// into the set's row buffer).  Caller holds the engine lock.
+int set_rows(hbh_commit_set* cs, hipStream_t s, size_t n, const uint32_t* part_idx, const uint32_t* xs,
+             std::vector<uint32_t>& slot) {
+  std::vector<uint32_t> np, nx;
+  slot.resize(n);
+  uint64_t last_key = ~(uint64_t)0;
+  uint32_t last_slot = 0;
+  for (size_t a = 0; a < n; a++) {
+    const uint64_t key = ((uint64_t)part_idx[a] << 32) | xs[a];
+    if (key != last_key) {  // consecutive acks of one (part, x) skip the map
+      auto it = cs->row_slot.emplace(key, (uint32_t)(cs->nrows + np.size()));
+      if (it.second) {
+        np.push_back(part_idx[a]);
+        nx.push_back(xs[a]);
+      }
+      last_key = key;
+      last_slot = it.first->second;
+    }
+    slot[a] = last_slot;
+  }
+  if (np.empty()) return HBH_OK;
+  const size_t row_bytes = hbl::bivar_rows_quad_bytes(1, cs->t);
+  const size_t first = cs->nrows;
+  int rc = grow_keep(s, &cs->rows, &cs->rows_cap, first * row_bytes, (first + np.size()) * row_bytes);
+  if (rc) {
+    for (size_t k = 0; k < np.size(); k++) cs->row_slot.erase(((uint64_t)np[k] << 32) | nx[k]);
+    return rc;
+  }
+  HBH_CHECK(cs->stage.ensure(np.size() * 8));
+  uint32_t* d_p = (uint32_t*)cs->stage.p;
+  HBH_CHECK(hipMemcpyAsync(d_p, np.data(), np.size() * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_p + np.size(), nx.data(), nx.size() * 4, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = cs->e->timer.begin(s, HBH_STAGE_CURVE, cs->e->profiling);
+  HBH_CHECK(hbl::bivar_row_quad(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(),
+                                (uint8_t*)cs->rows + first * row_bytes));
+  cs->e->timer.end(s, tm);
+  // the staged indices are read by the kernel: the host vectors die at return
+  HBH_CHECK(hipStreamSynchronize(s));
+  cs->nrows = first + np.size();
+  return HBH_OK;
+}
+
+// Acks in order of y (stable): the lanes of a wave then run the same small-scalar double-and-add.
+// y is a node index + 1, so a counting sort does it in O(n) (10^6 acks of a network-wide check).
+void order_by_y(size_t n, const uint32_t* ys, std::vector<uint32_t>& order) {
+  order.resize(n);
+  uint32_t ymax = 0;
+  for (size_t a = 0; a < n; a++) ymax = std::max(ymax, ys[a]);
+  if (ymax < (1u << 20)) {
+    std::vector<uint32_t> start((size_t)ymax + 2, 0);
+    for (size_t a = 0; a < n; a++) start[(size_t)ys[a] + 1]++;
+    for (size_t y = 1; y < start.size(); y++) start[y] += start[y - 1];
+    for (size_t a = 0; a < n; a++) order[start[ys[a]]++] = (uint32_t)a;
+    return;
+  }
+  for (size_t a = 0; a < n; a++) order[a] = (uint32_t)a;
+  std::stable_sort(order.begin(), order.end(), [ys](uint32_t i, uint32_t j) { return ys[i] < ys[j]; });
+}
+
+int check_parts(const hbh_commit_set* cs, size_t n, const uint32_t* part_idx) {
+  for (size_t a = 0; a < n; a++)
+    if (part_idx[a] >= cs->nparts) return fail(HBH_ERR_ARG, "part index out of range");
+  return HBH_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int hbh_commit_set_create(hbh_engine* e, int t, hbh_commit_set** out) {
+  if (!e || !out) return fail(HBH_ERR_ARG, "null pointer");
+  *out = nullptr;
+  int rc = check_t(t);
+  if (rc) return rc;
+  hbh_commit_set* cs = new hbh_commit_set();
+  cs->e = e;
+  cs->t = t;
+  cs->ncoef = (size_t)(t + 1) * (t + 2) / 2;
+  *out = cs;
+  return HBH_OK;
+}
+
+int hbh_commit_set_destroy(hbh_commit_set* cs) {
+  if (!cs) return HBH_OK;
+  hbh_engine* e = cs->e;
+  std::lock_guard<std::mutex> lk(e->mu);
+  (void)hipSetDevice(e->device);
+  (void)hipEventSynchronize(e->done);
+  (void)hipStreamSynchronize(e->stream);
+  if (cs->commits) (void)hipFree(cs->commits);
+  if (cs->rows) (void)hipFree(cs->rows);
+  cs->stage.release();
+  delete cs;
+  return HBH_OK;
+}
+
+int hbh_commit_set_add(hbh_commit_set* cs, size_t nparts, const uint8_t* commits, size_t* first) {
+  if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (first) *first = cs->nparts;
+  if (nparts == 0) return HBH_OK;
+  if (!commits) return fail(HBH_ERR_ARG, "null pointer");
+  if (cs->nparts + nparts > ((size_t)1 << 24)) return fail(HBH_ERR_ARG, "too many commitments");
+  hbh_engine* e = cs->e;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  int rc = begin_call(e, s);
+  if (rc) return rc;
+  const size_t cb = cs->ncoef * HBH_G1_BYTES;
+  rc = grow_keep(s, &cs->commits, &cs->commits_cap, cs->nparts * cb, (cs->nparts + nparts) * cb);
+  if (rc) return rc;
+  HBH_CHECK(hipMemcpyAsync((uint8_t*)cs->commits + cs->nparts * cb, commits, nparts * cb, hipMemcpyHostToDevice, s));
+  rc = end_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(hipStreamSynchronize(s));
+  cs->nparts += nparts;
+  return HBH_OK;
+}
+
+int hbh_commit_set_size(const hbh_commit_set* cs, size_t* nparts, size_t* nrows) {
+  if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (nparts) *nparts = cs->nparts;
+  if (nrows) *nrows = cs->nrows;
+  return HBH_OK;
+}
+
+int hbh_bivar_row_set(hbh_commit_set* cs, size_t nrow, const uint32_t* part_idx, const uint32_t* xs, uint8_t* out) {
+  if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (nrow == 0) return HBH_OK;
+  if (!part_idx || !xs || !out) return fail(HBH_ERR_ARG, "null pointer");
+  int rc = check_parts(cs, nrow, part_idx);
+  if (rc) return rc;
+  hbh_engine* e = cs->e;
+  const int t = cs->t;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  rc = begin_call(e, s);
+  if (rc) return rc;
+  const size_t nout = nrow * (t + 1);
+  HBH_CHECK(e->in_b.ensure(nrow * 8));
+  HBH_CHECK(e->out_x.ensure(nout * HBH_G1_BYTES));
+  uint32_t* d_p = (uint32_t*)e->in_b.p;
+  HBH_CHECK(hipMemcpyAsync(d_p, part_idx, nrow * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_p + nrow, xs, nrow * 4, hipMemcpyHostToDevice, s));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::bivar_row(s, (int)nrow, t, cs->commits, d_p, d_p + nrow, e->out_x.p));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, nout * HBH_G1_BYTES, hipMemcpyDeviceToHost, s));
+  rc = end_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* part_idx, const uint32_t* xs,
+                            const uint32_t* ys, const uint8_t* vals, uint8_t* verdicts) {
+  if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (nack == 0) return HBH_OK;
+  if (!part_idx || !xs || !ys || !vals || !verdicts) return fail(HBH_ERR_ARG, "null pointer");
+  if (nack > ((size_t)1 << 28)) return fail(HBH_ERR_ARG, "batch too large");
+  int rc = check_parts(cs, nack, part_idx);
+  if (rc) return rc;
+  std::vector<uint32_t> order;
+  order_by_y(nack, ys, order);
+  hbh_engine* e = cs->e;
+  const int t = cs->t;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  rc = begin_call(e, s);
+  if (rc) return rc;
+  std::vector<uint32_t> slot;
+  rc = set_rows(cs, s, nack, part_idx, xs, slot);
+  if (rc) return rc;
+  HBH_CHECK(e->in_b.ensure(nack * 12));
+  HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
+  HBH_CHECK(e->out_v.ensure(nack));
+  uint32_t* d_ro = (uint32_t*)e->in_b.p;
+  uint32_t* d_y = d_ro + nack;
+  uint32_t* d_ord = d_y + nack;
+  HBH_CHECK(hipMemcpyAsync(d_ro, slot.data(), nack * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_y, ys, nack * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(d_ord, order.data(), nack * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
+  rc = ensure_fbtab(e, s);
+  if (rc) return rc;
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, cs->rows, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
+                                  (uint8_t*)e->out_v.p, d_ord));
+  e->timer.end(s, tm);
+  HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, nack, hipMemcpyDeviceToHost, s));
+  rc = end_call(e, s);
+  if (rc) return rc;
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
+
+}  // extern "C"

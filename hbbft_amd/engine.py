@@ -21,6 +21,20 @@ def _u32(idx, n):
     return a, a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _fr_buf(vals, n):
+    """(owner, pointer) of n 32-byte LE scalars: ints, or already packed (bytes / uint8 array of
+    n * 32) -- a 10^6-ack call then skips the per-value packing."""
+    if isinstance(vals, np.ndarray):
+        a = np.ascontiguousarray(vals, dtype=np.uint8).reshape(-1)
+    elif isinstance(vals, (bytes, bytearray)):
+        a = np.frombuffer(bytes(vals), dtype=np.uint8)
+    else:
+        a = np.frombuffer(b"".join(int(v).to_bytes(32, "little") for v in vals), dtype=np.uint8)
+    if a.size != 32 * n:
+        raise ValueError("expected %d 32-byte scalars" % n)
+    return a, a.ctypes.data_as(ctypes.c_void_p)
+
+
 def _check_bivar(t, commits, part_idx):
     """Every BivarCommitment of a degree-t call holds (t+1)(t+2)/2 points, and every request names
     one of them: the kernels stride through the joined buffer by that count."""
@@ -296,6 +310,10 @@ class Engine:
         vp = ctypes.c_void_p
         check(self._l.hbh_g2_decompress_dev(self._h, vp(stream) if stream else None, n, vp(d_in), vp(d_out), vp(d_ok)))
 
+    def commit_set(self, t):
+        """An empty device-resident set of degree-t BivarCommitments (hbh_commit_set_create)."""
+        return CommitSet(self, t)
+
     def bivar_ack_check_dev(self, stream, nack, t, d_commits, nrow, d_row_part, d_row_x, d_row_of, d_ys, d_vals,
                             d_verdicts):
         vp = ctypes.c_void_p
@@ -364,6 +382,74 @@ def g1_abi_from_uncompressed(b):
     if _check_uncompressed(b, 96):
         return bytes(96)
     return b[0:48][::-1] + b[48:96][::-1]
+
+
+class CommitSet:
+    """Device-resident BivarCommitments of one degree (hbh_commit_set_*): a SyncKeyGen instance
+    uploads each Part's commitment once (ProposalState::commit, src/sync_key_gen.rs:254-262) and
+    checks rows (:496) and Acks (:542) against it by index; rows row(x) stay cached in HBM."""
+
+    def __init__(self, engine, t):
+        self._eng, self._l, self.t = engine, engine._l, int(t)
+        h = ctypes.c_void_p()
+        check(self._l.hbh_commit_set_create(engine._h, self.t, ctypes.byref(h)))
+        self._h = h
+
+    def add(self, commits):
+        """Append commitments ((t+1)(t+2)/2 ABI G1 points each); returns the first one's index."""
+        commits = list(commits)
+        _check_bivar(self.t, commits, [])
+        first = ctypes.c_size_t()
+        if not commits:
+            check(self._l.hbh_commit_set_add(self._h, 0, None, ctypes.byref(first)))
+            return first.value
+        keep = buf(_join([c for part in commits for c in part], G1_BYTES))
+        check(self._l.hbh_commit_set_add(self._h, len(commits), keep[1], ctypes.byref(first)))
+        return first.value
+
+    def size(self):
+        """(commitments held, rows cached)."""
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        check(self._l.hbh_commit_set_size(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def rows(self, part_idx, xs):
+        """BivarCommitment::row(x) per (set index, x), affine: as Engine.bivar_row."""
+        t, nrow = self.t, len(part_idx)
+        if nrow == 0:
+            return []
+        pa, ppa = _u32(part_idx, nrow)
+        xa, pxa = _u32(xs, nrow)
+        out = (ctypes.c_uint8 * (nrow * (t + 1) * G1_BYTES))()
+        check(self._l.hbh_bivar_row_set(self._h, nrow, ppa, pxa, ctypes.cast(out, ctypes.c_void_p)))
+        raw = bytes(out)
+        return [[raw[(r * (t + 1) + i) * G1_BYTES:(r * (t + 1) + i + 1) * G1_BYTES] for i in range(t + 1)]
+                for r in range(nrow)]
+
+    def ack_check(self, part_idx, xs, ys, vals):
+        """BivarCommitment::evaluate(x, y) == g1 * val per ack (set index, x, y, val): as
+        Engine.bivar_ack_check, without re-uploading the commitments."""
+        n = len(part_idx)
+        if n == 0:
+            return b""
+        pa, ppa = _u32(part_idx, n)
+        xa, pxa = _u32(xs, n)
+        ya, pya = _u32(ys, n)
+        vb = _fr_buf(vals, n)
+        out = (ctypes.c_uint8 * n)()
+        check(self._l.hbh_bivar_ack_check_set(self._h, n, ppa, pxa, pya, vb[1], ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._l.hbh_commit_set_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def g2_abi_from_uncompressed(b):

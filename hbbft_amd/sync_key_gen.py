@@ -172,6 +172,7 @@ class ProposalState:
         self.degree, self.commit = degree, list(commit)
         self.values = {}   # sender index + 1 -> Fr
         self.acks = set()  # sender indices
+        self.set_idx = None  # index of the commitment in the instance's device-resident set
 
     def equals_new(self, part):
         """``*state == ProposalState::new(commit)`` (sync_key_gen.rs:489): the derived PartialEq
@@ -242,6 +243,13 @@ class SyncKeyGen:
         self.parts = {}
         self.engine = engine
         self.threads = threads
+        self._sets = {}  # degree -> CommitSet: every Part's commitment uploaded to HBM once
+
+    def _commit_set(self, degree):
+        cs = self._sets.get(degree)
+        if cs is None:
+            cs = self._sets[degree] = self.engine.commit_set(degree)
+        return cs
 
     @classmethod
     def new(cls, our_id, sec_key, pub_keys, threshold, engine, rng=None, threads=0):
@@ -315,7 +323,13 @@ class SyncKeyGen:
             x = self.our_idx + 1
             commit_rows = [None] * len(new)
             for d, js in _by_degree(range(len(new)), lambda j: new[j][1].degree).items():
-                got = self.engine.bivar_row(d, [new[j][1].commit for j in js], list(range(len(js))), [x] * len(js))
+                # the commitments go to the device-resident set once; rows and later Ack checks
+                # name them by index
+                cs = self._commit_set(d)
+                first = cs.add([new[j][1].commit for j in js])
+                for k, j in enumerate(js):
+                    new[j][2].set_idx = first + k
+                got = cs.rows([first + k for k in range(len(js))], [x] * len(js))
                 for j, r in zip(js, got):
                     commit_rows[j] = r
             plain = _decrypt_batch(self.engine, self.sec_key, [p.rows[self.our_idx] for _, p, _ in new], self.threads)
@@ -416,17 +430,11 @@ class SyncKeyGen:
             vals = [de_val(b) if b is not None else None for b in plain]
             chk = [j for j, v in enumerate(vals) if v is not None]
             okmap = {}
-            # one hbh_bivar_ack_check per commitment degree; each part's commitment joined once
+            # one check per commitment degree against the device-resident commitments (uploaded
+            # once by handle_parts); only indices and values travel
             for d, js in _by_degree(chk, lambda j: new[j][2].degree).items():
-                commits, cidx = [], {}
-                for j in js:
-                    p = new[j][1].proposer_idx
-                    if p not in cidx:
-                        cidx[p] = len(commits)
-                        commits.append(new[j][2].commit)
-                ok = self.engine.bivar_ack_check(d, commits, [cidx[new[j][1].proposer_idx] for j in js],
-                                                 [self.our_idx + 1] * len(js), [new[j][0] + 1 for j in js],
-                                                 [vals[j] for j in js])
+                ok = self._commit_set(d).ack_check([new[j][2].set_idx for j in js], [self.our_idx + 1] * len(js),
+                                                   [new[j][0] + 1 for j in js], [vals[j] for j in js])
                 okmap.update(zip(js, ok))
             for j in range(len(new)):
                 if plain[j] is None:

@@ -201,6 +201,27 @@ int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, cons
                         const uint32_t* part_idx, const uint32_t* xs, const uint32_t* ys, const uint8_t* vals,
                         uint8_t* verdicts);
 
+/* Device-resident commitments.  A SyncKeyGen instance keeps every Part's BivarCommitment for its
+ * lifetime (ProposalState::commit, src/sync_key_gen.rs:254-262) and checks rows (:496) and Acks
+ * (:542) against it on every drain.  A commitment set holds such commitments (one degree t per set)
+ * in HBM, uploaded once, plus the Jacobian rows row(x) computed so far; calls name parts by their
+ * index in the set and upload only indices and values.
+ *   hbh_commit_set_create / _destroy: an empty set of degree t on `eng` (destroy waits for the
+ *     engine's work).
+ *   hbh_commit_set_add: append nparts commitments ((t+1)(t+2)/2 ABI G1 points each, coeff_pos
+ *     order); *first (may be NULL) = the set index of the first one.
+ *   hbh_commit_set_size: commitments and cached rows held.
+ *   hbh_bivar_row_set / hbh_bivar_ack_check_set: hbh_bivar_row / hbh_bivar_ack_check with part_idx
+ *     into the set (same outputs). */
+typedef struct hbh_commit_set hbh_commit_set;
+int hbh_commit_set_create(hbh_engine* eng, int t, hbh_commit_set** out);
+int hbh_commit_set_destroy(hbh_commit_set* cs);
+int hbh_commit_set_add(hbh_commit_set* cs, size_t nparts, const uint8_t* commits, size_t* first);
+int hbh_commit_set_size(const hbh_commit_set* cs, size_t* nparts, size_t* nrows);
+int hbh_bivar_row_set(hbh_commit_set* cs, size_t nrow, const uint32_t* part_idx, const uint32_t* xs, uint8_t* out);
+int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* part_idx, const uint32_t* xs,
+                            const uint32_t* ys, const uint8_t* vals, uint8_t* verdicts);
+
 /* Commitment::evaluate(x) = sum_j C_j x^j for n (commitment, x) requests; commits holds ncommits
  * Commitments of t+1 G1 points each, out = n G1 points.  PublicKeySet::public_key_share(i) is
  * evaluate(i + 1): NetworkInfo::new precomputes it for every node (src/network_info.rs:59-62), and

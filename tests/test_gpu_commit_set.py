@@ -1,0 +1,84 @@
+"""Device-resident commitment sets (hbh_commit_set_*, include/hbbft_hip.h): a SyncKeyGen instance's
+BivarCommitments uploaded once and checked by index (ProposalState::commit,
+src/sync_key_gen.rs:254-262, rows :496, Acks :542).
+
+* the set's rows and Ack verdicts equal the stateless hbh_bivar_row / hbh_bivar_ack_check on the
+  same commitments, across two appends and with rows cached by an earlier call;
+* configs[3] at network scale: all 100 nodes' acks (10^6 checks over 100 Parts of degree 33, 1/97
+  tampered) in one call equal the construction, and a sample equals the C oracle's
+  BivarCommitment::evaluate == g1 * val (oracle/c/bls_cpu.c)."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import bls12_381 as C
+from oracle import cbls
+from hbbft_amd._lib import HbhError
+from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
+
+pytestmark = pytest.mark.gpu
+R = C.R
+G1 = g1a(C.g1_uncompressed(C.G1_GEN))
+
+
+def cp(i, j):
+    return j * (j + 1) // 2 + i if i <= j else i * (i + 1) // 2 + j
+
+
+def f_eval(c, t, x, y):
+    return sum(c[cp(i, j)] * pow(x, i, R) * pow(y, j, R) for i in range(t + 1) for j in range(t + 1)) % R
+
+
+def test_commit_set_matches_stateless(engine):
+    rng = random.Random(61)
+    t, nparts = 4, 7
+    npos = (t + 1) * (t + 2) // 2
+    coefs = [[rng.randrange(R) for _ in range(npos)] for _ in range(nparts)]
+    flat = engine.g1_mul_gen([c for cs in coefs for c in cs])
+    commits = [flat[p * npos:(p + 1) * npos] for p in range(nparts)]
+    cs = engine.commit_set(t)
+    assert cs.add(commits[:3]) == 0 and cs.add(commits[3:]) == 3 and cs.size() == (nparts, 0)
+    rp = [rng.randrange(nparts) for _ in range(20)]
+    rx = [rng.randrange(1, 50) for _ in range(20)]
+    assert cs.rows(rp, rx) == engine.bivar_row(t, commits, rp, rx)
+    acks = [(rng.randrange(nparts), rng.randrange(1, 9), rng.randrange(1, 60)) for _ in range(300)]
+    vals = [f_eval(coefs[p], t, x, y) for p, x, y in acks]
+    bad = set(range(0, len(acks), 7))
+    vals = [(v + 1) % R if a in bad else v for a, v in enumerate(vals)]
+    args = ([a[0] for a in acks], [a[1] for a in acks], [a[2] for a in acks], vals)
+    want = bytes(0 if a in bad else 1 for a in range(len(acks)))
+    assert engine.bivar_ack_check(t, commits, *args) == want
+    got = cs.ack_check(*args)
+    assert got == want
+    nrows = cs.size()[1]
+    assert 0 < nrows <= nparts * 8
+    assert cs.ack_check(*args) == want and cs.size()[1] == nrows  # rows served from the cache
+    packed = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in vals), dtype=np.uint8).reshape(-1, 32)
+    assert cs.ack_check(np.array(args[0]), np.array(args[1]), np.array(args[2]), packed) == want
+    with pytest.raises(HbhError):
+        cs.ack_check([nparts], [1], [1], [0])
+    with pytest.raises(ValueError):
+        cs.add([commits[0][:-1]])
+    cs.close()
+
+
+def test_config3_network_acks(engine):
+    """configs[3] network-wide: 10^6 Ack checks (every node x of 100 checks the acks of all 100
+    senders for all 100 Parts) in one call against resident commitments."""
+    import bench
+    n_nodes, t = 100, 33
+    commits, pidx, xs, ys, vals, expected = bench.dkg_workload(engine, 100, n_nodes, t, range(1, n_nodes + 1))
+    assert len(expected) == n_nodes ** 3
+    cs = engine.commit_set(t)
+    cs.add(commits)
+    got = cs.ack_check(pidx, xs, ys, vals)
+    assert cs.size() == (n_nodes, n_nodes * n_nodes)
+    assert got == expected
+    rng = random.Random(62)
+    sample = sorted(rng.sample(range(len(expected)), 20)) + [0, 97, len(expected) - 1]
+    for a in sample:
+        lhs = cbls.bivar_evaluate(t, commits[int(pidx[a])], int(xs[a]), int(ys[a]))
+        rhs = cbls.g1_mul(G1, int.from_bytes(bytes(vals[a]), "little"))
+        assert (lhs == rhs) == bool(got[a]), a
+    cs.close()

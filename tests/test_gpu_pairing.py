@@ -94,9 +94,8 @@ def test_empty_batch(eng):
 
 
 def test_implementations_agree_random_batch(engine):
-    """A 1,003-check random batch (valid, swapped, infinity, ragged vs the 10-checks-per-wave
-    lane-cooperative and 128-checks-per-workgroup lane-pair layouts): all implementations and the C
-    oracle agree on every verdict."""
+    """A 1,003-check random batch (valid, swapped, infinity, ragged vs the 128-checks-per-workgroup
+    lane-pair layout): both implementations and the C oracle agree on every verdict."""
     import random
     from oracle import cbls
     rng = random.Random(7)
@@ -119,21 +118,17 @@ def test_implementations_agree_random_batch(engine):
         P.append(pk), S.append(sig), D.append(d)
     for i in range(0, n, 97):
         want.append((i, cbls.verify_g2(P[i], S[i], hs[D[i]])))
-    engine.set_pairing_impl(1)
-    v1 = engine.verify_sig_shares(P, S, hs, D)
-    engine.set_pairing_impl(2)
-    v2 = engine.verify_sig_shares(P, S, hs, D)
-    engine.set_pairing_impl(4)
-    v0 = engine.verify_sig_shares(P, S, hs, D)
-    engine.set_pairing_impl(5)
-    v5 = engine.verify_sig_shares(P, S, hs, D)
-    engine.set_pairing_impl(3)
-    assert v1 == v0
-    assert v2 == v0
+    try:
+        engine.set_pairing_impl(4)
+        v0 = engine.verify_sig_shares(P, S, hs, D)
+        engine.set_pairing_impl(5)
+        v5 = engine.verify_sig_shares(P, S, hs, D)
+    finally:
+        engine.set_pairing_impl(3)
     assert v5 == v0
     for i, w in want:
-        assert v1[i] == int(w), i
-    assert sum(v1) == sum(1 for i in range(n) if i % 11 not in (3, 5))
+        assert v0[i] == int(w), i
+    assert sum(v0) == sum(1 for i in range(n) if i % 11 not in (3, 5))
 
 
 def test_verify_signatures_public_key_verify(eng):
