@@ -39,6 +39,7 @@ R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 # Roofline denominator: measured v_mad_u64_u32 throughput on one MI355X
 # (tools/ubench_v2.hip, profiles/r02/ubench_v2_mad.txt: 8 independent chains per wave), by waves
 # per SIMD; the theoretical half-rate figure is reported beside it.
+ACK_LANE_MIN = 65536                            # HBH_ACK_LANE_MIN (include/hbbft_hip.h)
 MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
@@ -400,6 +401,10 @@ def main():
     ap.add_argument("--impl", choices=["pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
+    ap.add_argument("--ack-impl", choices=["auto", "quad", "lane"], default="auto",
+                    help="dkg workload: Ack-check kernel (hbh_engine_set_ack_impl)")
+    ap.add_argument("--dkg-nodes", type=int, default=0,
+                    help="dkg workload, network scope: checking nodes (0 = all 100; 10,000 acks each)")
     ap.add_argument("--dkg-scope", choices=["network", "node"], default="network",
                     help="dkg workload: the whole network's 10^6 ack checks split over the ranks, or one node's "
                          "10,000 per rank")
@@ -735,9 +740,10 @@ def run_dkg(args, eng, world, rank, dev):
     npos = (t + 1) * (t + 2) // 2
     network = args.dkg_scope == "network"
     if network:
-        nodes = [x for x in range(1, n_nodes + 1) if (x - 1) % world == rank]
+        nodes = [x for x in range(1, (args.dkg_nodes or n_nodes) + 1) if (x - 1) % world == rank]
     else:
         nodes = [rank + 1]
+    eng.set_ack_impl({"auto": 0, "quad": 1, "lane": 2}[args.ack_impl])
     t0 = time.perf_counter()
     commits, pidx, xs, ys, vals, expected = dkg_workload(eng, 100, n_nodes, t, nodes)
     gen_s = time.perf_counter() - t0
@@ -769,6 +775,19 @@ def run_dkg(args, eng, world, rank, dev):
     row_ms, _ = eng.stage_time(STAGE_CURVE)
     eng.set_profiling(False)
     cs2.close()
+    # BivarPoly::commitment (src/sync_key_gen.rs:346-357): the 595-point commitment of one Part, and
+    # of all 100 Parts in one call, on the fixed-base comb table (hbh_g1_mul_gen); host-to-host
+    crng = random.Random(7)
+    commit_ms = {}
+    for k in (1, n_nodes):
+        sc = [crng.randrange(R_ORDER) for _ in range(k * npos)]
+        eng.g1_mul_gen(sc[:8])
+        ts_ = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            eng.g1_mul_gen(sc)
+            ts_.append((time.perf_counter() - t0) * 1e3)
+        commit_ms[k] = statistics.median(ts_)
     ms = _max_over_ranks(dev_ms, world, dev)
     host_ms = _max_over_ranks(statistics.median(times), world, dev)
     per_rank = gather_per_rank({"rank": rank, "device_ms": dev_ms, "host_ms": statistics.median(times), "ok": ok,
@@ -778,8 +797,10 @@ def run_dkg(args, eng, world, rank, dev):
     if rank == 0:
         ops = [workcount.bivar_ack(t, y) for y in range(1, n_nodes + 1)]
         op = (sum(o[0] for o in ops) / n_nodes, sum(o[1] for o in ops) / n_nodes)
-        waves = 4 * nack / 64 / 1024
-        main_k = roofline_entry("hbs::k_bivar_check_quad", dev_n, dev_ms, nack, op, "ack check", waves)
+        lane = args.ack_impl == "lane" or (args.ack_impl == "auto" and nack >= ACK_LANE_MIN)
+        kname = "hb::k_bivar_check" if lane else "hbs::k_bivar_check_quad"
+        waves = (1 if lane else 4) * nack / 64 / 1024
+        main_k = roofline_entry(kname, dev_n, dev_ms, nack, op, "ack check", waves)
         line = {
             "metric": "SyncKeyGen ack checks/sec (%s), N=100 t=33" % ("whole network" if network else "whole node set"),
             "value": total / (ms / 1e3), "unit": "acks/s", "n_gpus": world, "steps": nsteps, "warmup": 1,
@@ -795,10 +816,14 @@ def run_dkg(args, eng, world, rank, dev):
                                  "resident in HBM (commitment set); host_to_host_ms: the whole call incl. the "
                                  "upload of indices and values"},
             "host_to_host_ms": host_ms, "row_build_ms": row_ms, "rows": len(nodes) * n_nodes,
+            "bivar_commitment_ms": {"1 part (595 points)": commit_ms[1], "100 parts (59,500 points)": commit_ms[n_nodes],
+                                    "note": "BivarPoly::commitment on the comb table (hbh_g1_mul_gen), host-to-host"},
             "data_gen_s": round(gen_s, 2), "verdicts_ok": ok, "per_rank": per_rank,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
-                             traffic=pmc_traffic("hbs::k_bivar_check_quad"),
-                             note="four lanes per ack (lane quads); %.1f waves per SIMD" % waves),
+                             note="%s; %.1f waves per SIMD launched" % (
+                                 "one lane per ack on affine rows" if lane else "four lanes per ack (lane quads)",
+                                 waves)),
+            "ack_impl": kname,
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline_dkg(t, commits, pidx, xs, ys, vals, expected, eng)

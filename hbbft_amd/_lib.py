@@ -48,6 +48,7 @@ SIGNATURES = [
     ("hbh_bivar_row_set", _I, [_P, _SZ, _P, _P, _P]),
     ("hbh_bivar_ack_check_set", _I, [_P, _SZ, _P, _P, _P, _P, _P]),
     ("hbh_engine_set_pairing_impl", _I, [_P, _I]),
+    ("hbh_engine_set_ack_impl", _I, [_P, _I]),
     ("hbh_engine_set_profiling", _I, [_P, _I]),
     ("hbh_engine_stage_time", _I, [_P, _I, _c.POINTER(_c.c_double), _c.POINTER(_I)]),
     # device-resident variants
@@ -83,6 +84,7 @@ SIGNATURES = [
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
 IMPL_AUTO, IMPL_PAIR, IMPL_WAVE = 3, 4, 5   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)
+ACK_AUTO, ACK_QUAD, ACK_LANE = 0, 1, 2        # HBH_ACK_*
 
 _lib = None
 

@@ -88,6 +88,7 @@ struct hbh_engine {
   std::mutex mu;
   bool profiling = false;
   int impl = HBH_IMPL_AUTO;  // pairing implementation (hbh_engine_set_pairing_impl)
+  int ack_impl = HBH_ACK_AUTO;  // Ack-check kernel of commitment sets (hbh_engine_set_ack_impl)
   StageTimer timer;
   // Completion of the last call's device work on whichever stream it ran.  Every call waits for it
   // on its own stream before touching the engine-owned workspaces, so a _dev call on a caller
@@ -379,6 +380,15 @@ int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
     return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;
+  return HBH_OK;
+}
+
+int hbh_engine_set_ack_impl(hbh_engine* e, int impl) {
+  if (!e) return fail(HBH_ERR_ARG, "null engine");
+  if (impl != HBH_ACK_AUTO && impl != HBH_ACK_QUAD && impl != HBH_ACK_LANE)
+    return fail(HBH_ERR_ARG, "unknown Ack-check implementation");
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->ack_impl = impl;
   return HBH_OK;
 }
 
@@ -1183,11 +1193,16 @@ struct hbh_commit_set {
   size_t nparts = 0;
   void* commits = nullptr;  // nparts * ncoef ABI G1 points
   size_t commits_cap = 0;   // bytes
-  std::unordered_map<uint64_t, uint32_t> row_slot;  // (part << 32 | x) -> row
-  size_t nrows = 0;
-  void* rows = nullptr;     // nrows Jacobian rows (hbl::bivar_rows_quad_bytes(1, t) each)
-  size_t rows_cap = 0;      // bytes
-  DevBuf stage;             // indices of rows computed by a call
+  // cached rows row(x), two layouts: [0] Jacobian signed-limb rows of the lane-quad check
+  // (hbl::bivar_rows_quad_bytes(1, t) each), [1] affine ABI rows of the one-lane check
+  // ((t + 1) G1 points each)
+  struct Rows {
+    std::unordered_map<uint64_t, uint32_t> slot;  // (part << 32 | x) -> row
+    size_t n = 0;
+    void* p = nullptr;
+    size_t cap = 0;  // bytes
+  } rows[2];
+  DevBuf stage;      // indices of rows computed by a call
 };
 
 namespace {
@@ -1207,8 +1222,9 @@ int grow_keep(hipStream_t s, void** p, size_t* cap, size_t used, size_t want) {
 
 // Row slots for n (part, x) requests; rows not cached yet are computed on stream s (k_bivar_row_quad
 // into the set's row buffer).  Caller holds the engine lock.
-int set_rows(hbh_commit_set* cs, hipStream_t s, size_t n, const uint32_t* part_idx, const uint32_t* xs,
+int set_rows(hbh_commit_set* cs, hipStream_t s, bool affine, size_t n, const uint32_t* part_idx, const uint32_t* xs,
              std::vector<uint32_t>& slot) {
+  hbh_commit_set::Rows& R = cs->rows[affine ? 1 : 0];
   std::vector<uint32_t> np, nx;
   slot.resize(n);
   uint64_t last_key = ~(uint64_t)0;
@@ -1216,7 +1232,7 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, size_t n, const uint32_t* part_i
   for (size_t a = 0; a < n; a++) {
     const uint64_t key = ((uint64_t)part_idx[a] << 32) | xs[a];
     if (key != last_key) {  // consecutive acks of one (part, x) skip the map
-      auto it = cs->row_slot.emplace(key, (uint32_t)(cs->nrows + np.size()));
+      auto it = R.slot.emplace(key, (uint32_t)(R.n + np.size()));
       if (it.second) {
         np.push_back(part_idx[a]);
         nx.push_back(xs[a]);
@@ -1227,11 +1243,11 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, size_t n, const uint32_t* part_i
     slot[a] = last_slot;
   }
   if (np.empty()) return HBH_OK;
-  const size_t row_bytes = hbl::bivar_rows_quad_bytes(1, cs->t);
-  const size_t first = cs->nrows;
-  int rc = grow_keep(s, &cs->rows, &cs->rows_cap, first * row_bytes, (first + np.size()) * row_bytes);
+  const size_t row_bytes = affine ? (size_t)(cs->t + 1) * HBH_G1_BYTES : hbl::bivar_rows_quad_bytes(1, cs->t);
+  const size_t first = R.n;
+  int rc = grow_keep(s, &R.p, &R.cap, first * row_bytes, (first + np.size()) * row_bytes);
   if (rc) {
-    for (size_t k = 0; k < np.size(); k++) cs->row_slot.erase(((uint64_t)np[k] << 32) | nx[k]);
+    for (size_t k = 0; k < np.size(); k++) R.slot.erase(((uint64_t)np[k] << 32) | nx[k]);
     return rc;
   }
   HBH_CHECK(cs->stage.ensure(np.size() * 8));
@@ -1239,12 +1255,15 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, size_t n, const uint32_t* part_i
   HBH_CHECK(hipMemcpyAsync(d_p, np.data(), np.size() * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(d_p + np.size(), nx.data(), nx.size() * 4, hipMemcpyHostToDevice, s));
   hipEvent_t tm = cs->e->timer.begin(s, HBH_STAGE_CURVE, cs->e->profiling);
-  HBH_CHECK(hbl::bivar_row_quad(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(),
-                                (uint8_t*)cs->rows + first * row_bytes));
+  void* dst = (uint8_t*)R.p + first * row_bytes;
+  if (affine)
+    HBH_CHECK(hbl::bivar_row(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(), dst));
+  else
+    HBH_CHECK(hbl::bivar_row_quad(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(), dst));
   cs->e->timer.end(s, tm);
   // the staged indices are read by the kernel: the host vectors die at return
   HBH_CHECK(hipStreamSynchronize(s));
-  cs->nrows = first + np.size();
+  R.n = first + np.size();
   return HBH_OK;
 }
 
@@ -1295,7 +1314,8 @@ int hbh_commit_set_destroy(hbh_commit_set* cs) {
   (void)hipEventSynchronize(e->done);
   (void)hipStreamSynchronize(e->stream);
   if (cs->commits) (void)hipFree(cs->commits);
-  if (cs->rows) (void)hipFree(cs->rows);
+  for (auto& R : cs->rows)
+    if (R.p) (void)hipFree(R.p);
   cs->stage.release();
   delete cs;
   return HBH_OK;
@@ -1327,7 +1347,7 @@ int hbh_commit_set_add(hbh_commit_set* cs, size_t nparts, const uint8_t* commits
 int hbh_commit_set_size(const hbh_commit_set* cs, size_t* nparts, size_t* nrows) {
   if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
   if (nparts) *nparts = cs->nparts;
-  if (nrows) *nrows = cs->nrows;
+  if (nrows) *nrows = cs->rows[0].n + cs->rows[1].n;
   return HBH_OK;
 }
 
@@ -1377,8 +1397,11 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
   hipStream_t s = e->stream;
   rc = begin_call(e, s);
   if (rc) return rc;
+  // lane quads (four lanes per ack, one wave per SIMD) for latency; one lane per ack on affine
+  // rows (two waves per SIMD, mixed additions) for throughput
+  const bool lane = e->ack_impl == HBH_ACK_LANE || (e->ack_impl == HBH_ACK_AUTO && nack >= HBH_ACK_LANE_MIN);
   std::vector<uint32_t> slot;
-  rc = set_rows(cs, s, nack, part_idx, xs, slot);
+  rc = set_rows(cs, s, lane, nack, part_idx, xs, slot);
   if (rc) return rc;
   HBH_CHECK(e->in_b.ensure(nack * 12));
   HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
@@ -1393,8 +1416,12 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, cs->rows, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
-                                  (uint8_t*)e->out_v.p, d_ord));
+  if (lane)
+    HBH_CHECK(hbl::bivar_check(s, (int)nack, t, cs->rows[1].p, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
+                               (uint8_t*)e->out_v.p, d_ord));
+  else
+    HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, cs->rows[0].p, d_ro, d_y, (const uint32_t*)e->in_c.p,
+                                    e->fbtab.p, (uint8_t*)e->out_v.p, d_ord));
   e->timer.end(s, tm);
   HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, nack, hipMemcpyDeviceToHost, s));
   rc = end_call(e, s);

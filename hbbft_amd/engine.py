@@ -327,6 +327,10 @@ class Engine:
         kernel).  0, 1, 2 are retired implementations (HBH_ERR_ARG)."""
         check(self._l.hbh_engine_set_pairing_impl(self._h, int(impl)))
 
+    def set_ack_impl(self, impl):
+        """HBH_ACK_*: 0 = auto (default), 1 = lane quads, 2 = one lane per ack (commitment sets)."""
+        check(self._l.hbh_engine_set_ack_impl(self._h, int(impl)))
+
     # ------------------------------------------------------------ profiling
     def set_profiling(self, on):
         check(self._l.hbh_engine_set_profiling(self._h, 1 if on else 0))

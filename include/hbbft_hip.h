@@ -309,6 +309,16 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_WAVE 5
 #define HBH_AUTO_WAVE_MAX 8192
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
+/* Ack-check kernel of hbh_bivar_ack_check_set: HBH_ACK_QUAD (k_bivar_check_quad: four lanes per ack
+ * split each G1 operation, Jacobian rows -- latency), HBH_ACK_LANE (k_bivar_check: one lane per ack,
+ * affine rows and mixed additions -- throughput), HBH_ACK_AUTO (default: LANE from HBH_ACK_LANE_MIN
+ * acks per call; measured crossover ~50,000 acks, profiles/r03/ack_kernel_sweep.txt: 40,000 acks
+ * quad 6.4 / lane 7.0 ms, 160,000 acks 18.9 / 13.1 ms, 10^6 acks 112 / 53 ms).  Same verdicts. */
+#define HBH_ACK_AUTO 0
+#define HBH_ACK_QUAD 1
+#define HBH_ACK_LANE 2
+#define HBH_ACK_LANE_MIN 65536
+int hbh_engine_set_ack_impl(hbh_engine* eng, int impl);
 
 /* ---------------------------------------------------------------- profiling
  * With profiling on, the engine records HIP events around each stage's kernels on the stream they

@@ -14,7 +14,7 @@ import pytest
 
 from oracle import bls12_381 as C
 from oracle import cbls
-from hbbft_amd._lib import HbhError
+from hbbft_amd._lib import ACK_AUTO, ACK_LANE, ACK_QUAD, HbhError
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
 
 pytestmark = pytest.mark.gpu
@@ -49,13 +49,17 @@ def test_commit_set_matches_stateless(engine):
     args = ([a[0] for a in acks], [a[1] for a in acks], [a[2] for a in acks], vals)
     want = bytes(0 if a in bad else 1 for a in range(len(acks)))
     assert engine.bivar_ack_check(t, commits, *args) == want
-    got = cs.ack_check(*args)
-    assert got == want
-    nrows = cs.size()[1]
-    assert 0 < nrows <= nparts * 8
-    assert cs.ack_check(*args) == want and cs.size()[1] == nrows  # rows served from the cache
     packed = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in vals), dtype=np.uint8).reshape(-1, 32)
-    assert cs.ack_check(np.array(args[0]), np.array(args[1]), np.array(args[2]), packed) == want
+    try:
+        for impl in (ACK_QUAD, ACK_LANE):  # lane quads on Jacobian rows, one lane on affine rows
+            engine.set_ack_impl(impl)
+            assert cs.ack_check(*args) == want, impl
+            nrows = cs.size()[1]
+            assert 0 < nrows <= 2 * nparts * 8
+            assert cs.ack_check(*args) == want and cs.size()[1] == nrows  # rows served from the cache
+            assert cs.ack_check(np.array(args[0]), np.array(args[1]), np.array(args[2]), packed) == want
+    finally:
+        engine.set_ack_impl(ACK_AUTO)
     with pytest.raises(HbhError):
         cs.ack_check([nparts], [1], [1], [0])
     with pytest.raises(ValueError):
@@ -72,9 +76,14 @@ def test_config3_network_acks(engine):
     assert len(expected) == n_nodes ** 3
     cs = engine.commit_set(t)
     cs.add(commits)
-    got = cs.ack_check(pidx, xs, ys, vals)
+    got = cs.ack_check(pidx, xs, ys, vals)   # AUTO: one lane per ack at this size
     assert cs.size() == (n_nodes, n_nodes * n_nodes)
     assert got == expected
+    try:
+        engine.set_ack_impl(ACK_QUAD)
+        assert cs.ack_check(pidx[:200000], xs[:200000], ys[:200000], vals[:200000]) == expected[:200000]
+    finally:
+        engine.set_ack_impl(ACK_AUTO)
     rng = random.Random(62)
     sample = sorted(rng.sample(range(len(expected)), 20)) + [0, 97, len(expected) - 1]
     for a in sample:
