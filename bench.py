@@ -401,6 +401,8 @@ def main():
     ap.add_argument("--impl", choices=["pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
+    ap.add_argument("--epoch-coins", choices=["ba", "synthetic"], default="ba",
+                    help="epoch workload: coins from Binary Agreement instances or one ThresholdSign each")
     ap.add_argument("--ack-impl", choices=["auto", "quad", "lane"], default="auto",
                     help="dkg workload: Ack-check kernel (hbh_engine_set_ack_impl)")
     ap.add_argument("--dkg-nodes", type=int, default=0,
@@ -868,6 +870,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
     keys = NetworkKeys(eng, n, f, rng)
     t0 = time.time()
     traces = [EpochTrace.generate(eng, keys, rng, hb_epoch=e, proposal_bytes=1000) for e in range(args.warmup + args.steps)]
+    if args.epoch_coins == "ba":  # coins from Binary Agreement instances (future-epoch queue, per-window combines)
+        for tr in traces:
+            tr.with_ba(eng, rng, extra=0.0)
     log("generated %d epoch traces in %.1f s" % (len(traces), time.time() - t0))
     ok = True
     for tr in traces[:args.warmup]:
@@ -885,6 +890,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
     eng.set_profiling(False)
     for tr, r in zip(traces[args.warmup:], results):
         ok = ok and r.plaintexts == tr.proposals and len(r.coins) == len(tr.coin_docs)
+        if args.epoch_coins == "ba":
+            ok = ok and r.ba_decisions == tr.ba.decision and r.ba_coins == tr.ba.coins
     ms = _max_over_ranks(wall * 1e3 / args.steps, world, dev)
     if rank == 0:
         drained = sum(r.checks_gpu for r in results)
@@ -901,6 +908,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
                     "1/64 forged shares); messages in random order",
             "config": {"workload": "HoneyBadger epoch crypto trace, BASELINE configs[4]", "n_nodes": n, "f": f,
                        "coins_per_epoch": len(traces[0].coin_docs), "window": args.window,
+                       "coins_from": ("BinaryAgreementCoin instances (epochs 0-2, coin shares through the future-epoch "
+                                      "queue, combines deferred per window)" if args.epoch_coins == "ba"
+                                      else "synthetic: one ThresholdSign per BA instance at epoch 2"),
                        "pipelined_drains": not args.no_pipeline,
                        "parallelism": "one node per rank x%d" % world,
                        "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},

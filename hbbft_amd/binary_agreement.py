@@ -14,10 +14,17 @@ Conf / Term vote counting).  Their outcome -- the aux values an epoch's SBV broa
 Conf round -- is handed in by the driver (``sbv_output``, ``conf_round_complete``) at the points where
 the reference's handle_sbvb_step (:301-324) and try_finish_conf_round (:469-480) act on it.
 """
-from .honey_badger import coin_document
-from .protocol import Fault, ProtocolError, Step, ThresholdSign, signature_parity
+import struct
 
-__all__ = ["BinaryAgreementCoin", "MAX_FUTURE_EPOCHS"]
+from .protocol import Deferred, Fault, ProtocolError, Step, ThresholdSign, signature_parity
+
+__all__ = ["BinaryAgreementCoin", "MAX_FUTURE_EPOCHS", "coin_document"]
+
+
+def coin_document(hb_id, hb_epoch, proposer_idx, ba_epoch):
+    """bincode of ((BaSessionId{subset_id: EpochId{hb_id, epoch}, proposer_idx}), ba_epoch): the
+    ThresholdSign document of a BA coin (binary_agreement.rs:442; subset.rs:182-185)."""
+    return struct.pack("<QQIQ", hb_id, hb_epoch, proposer_idx, ba_epoch)
 
 MAX_FUTURE_EPOCHS = 1000  # BinaryAgreement::new (binary_agreement.rs:214)
 
@@ -42,6 +49,8 @@ class BinaryAgreementCoin:
         self.incoming = {}   # epoch -> {sender: share}: the incoming_queue of future epochs
         self.queued = 0      # messages that went through the future-epoch queue
         self.coins = {}      # epoch -> coin value (threshold coins only)
+        self.signatures = {} # epoch -> combined coin signature
+        self.pending = None  # a deferred coin combine (BatchVerifier recording mode): resolve_pending
         self.coin_decided, self.coin_value, self.ts = self._coin_state()
 
     # ------------------------------------------------------------ coin state (:437-448)
@@ -90,10 +99,31 @@ class BinaryAgreementCoin:
         step = Step(fault_log=[Fault(f.node_id, "CoinFault:" + f.kind) for f in ts_step.fault_log],
                     messages=[(target, (epoch, share)) for target, share in ts_step.messages])
         if ts_step.output and not self.coin_decided:
-            self.coin_decided, self.coin_value = True, signature_parity(ts_step.output[0])
+            sig = ts_step.output[0]
+            self.signatures[epoch] = sig
+            if isinstance(sig, Deferred):  # combined in the driver's next batch: resolve_pending
+                self.pending = sig
+                return step
+            self.coin_decided, self.coin_value = True, signature_parity(sig)
             self.coins[epoch] = self.coin_value
             step.extend(self.try_update_epoch())
         return step
+
+    def resolve_pending(self):
+        """The driver flushed the deferred combines (BatchVerifier.flush_combines): the coin of the
+        current epoch becomes the signature's parity and the epoch may advance (its queued shares are
+        replayed).  A failed combine is the reference's Err from the call that completed the coin
+        (threshold_sign.rs:249-270 through Error::HandleThresholdSign)."""
+        d, self.pending = self.pending, None
+        if d is None:
+            return Step()
+        if not d.ok:
+            kind = "VerificationFailed" if d.result[1] == 0 else "CombineAndVerifySigCrypto"
+            raise ProtocolError("HandleThresholdSign", kind)
+        self.signatures[self.epoch] = d.result[0]
+        self.coin_decided, self.coin_value = True, signature_parity(d.result[0])
+        self.coins[self.epoch] = self.coin_value
+        return self.try_update_epoch()
 
     # ------------------------------------------------------------ SBV broadcast / Conf round outcomes
     def sbv_output(self, values):

@@ -132,7 +132,7 @@ HP_D Fp wv_mul(const Fp (&x)[K], const Fp (&y)[K]) {
       col += acc[c];
     }
     if (k < NL) {
-      m[k] = (int32_t)(((uint32_t)col * NP0) & (uint32_t)MASK28);
+      m[k] = mont_digit(col);
       col += (int64_t)m[k] * (int32_t)P_L[0];
     } else {
       r.l[k - NL] = (int32_t)col & MASK28;

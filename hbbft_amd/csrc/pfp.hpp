@@ -88,7 +88,7 @@ HS_MULFN Fp h_mul_l(HS_P14(x), HS_P14(y)) {
       }
     }
     if (HS_NCH > 1) acc += c2;
-    m[k] = (int32_t)(((uint32_t)acc * NP0) & (uint32_t)MASK28);
+    m[k] = mont_digit(acc);
     acc += (int64_t)m[k] * (int32_t)P_L[0];
     acc >>= 28;
   }

@@ -69,6 +69,11 @@ struct Fp2 {
   Fp c0, c1;
 };
 
+// Montgomery digit m = low 28 bits of (column * -p^-1).  (v_mul_lo_u32 issues at full rate on gfx950,
+// tools/ubench_mullo.hip: 30.8 T ops/s; computing it with v_mad_u64_u32 instead measured slower:
+// sign 22.87 -> 23.01 ms, profiles/r03/ab_mad_digit.txt.)
+HS_HD int32_t mont_digit(int64_t col) { return (int32_t)(((uint32_t)col * NP0) & (uint32_t)MASK28); }
+
 HS_HD Fp fp_zero() {
   Fp r;
 #pragma unroll
@@ -114,7 +119,7 @@ HS_MULFN Fp fp_mul_l(HS_P14(x), HS_P14(y)) {
       }
     }
     if (HS_NCH > 1) acc += red;
-    m[k] = (int32_t)(((uint32_t)acc * NP0) & (uint32_t)MASK28);
+    m[k] = mont_digit(acc);
     acc += (int64_t)m[k] * (int32_t)P_L[0];
     acc >>= 28;
   }
@@ -162,7 +167,7 @@ HS_MULFN Fp fp_sqr_l(HS_P14(x)) {
       }
     }
     if (HS_NCH > 1) acc += red;
-    m[k] = (int32_t)(((uint32_t)acc * NP0) & (uint32_t)MASK28);
+    m[k] = mont_digit(acc);
     acc += (int64_t)m[k] * (int32_t)P_L[0];
     acc >>= 28;
   }

@@ -31,6 +31,7 @@ import time
 
 from . import hoststage
 from . import wire
+from .binary_agreement import BinaryAgreementCoin, coin_document
 from .protocol import BatchVerifier, Ciphertext, Deferred, Fault, NetworkInfo, ProtocolError, Step, \
     ThresholdDecrypt, ThresholdSign, signature_parity
 from .sync_key_gen import G1_GEN, G2_GEN, R_ORDER
@@ -38,9 +39,6 @@ from .sync_key_gen import G1_GEN, G2_GEN, R_ORDER
 __all__ = ["NetworkKeys", "EpochTrace", "coin_document", "run_epoch", "EpochResult"]
 
 
-def coin_document(hb_id, hb_epoch, proposer_idx, ba_epoch):
-    """bincode of ((BaSessionId{subset_id: EpochId{hb_id, epoch}, proposer_idx}), ba_epoch)."""
-    return struct.pack("<QQIQ", hb_id, hb_epoch, proposer_idx, ba_epoch)
 
 
 def _poly_eval(coeffs, x):
@@ -165,6 +163,7 @@ class EpochTrace:
         tr = cls(keys, hb_epoch, proposals, cts, coin_docs, coin_shares, dec_shares, coin_msgs, dec_msgs)
         tr.bad = bad
         tr.hashes = hashes
+        tr.adv = adv
         return tr
 
 
@@ -190,6 +189,82 @@ def _serialize(trace, corrupt=()):
 
 EpochTrace.serialize = _serialize
 
+BOTH = frozenset((False, True))
+
+
+class BaTrace:
+    """The Binary Agreement side of an epoch for node ``our``: per BA instance (proposer p) the
+    aux values its SBV broadcast outputs in each epoch (``sched[p][e]``), the coin documents and the
+    other nodes' coin shares of every threshold-coin epoch on the instance's path (``docs[(p, e)]``,
+    ``shares[(p, e, j)]``), the share messages in delivery order (``msgs``: (p, e, j)) and, per
+    (p, e), the message positions after which our SBV output and our Conf round complete
+    (``release``).  Shares of an epoch our instance has not reached go through its future-epoch
+    queue (binary_agreement.rs:245-266)."""
+
+    def __init__(self):
+        self.sched, self.docs, self.shares, self.msgs, self.release = {}, {}, {}, [], {}
+        self.decision, self.coins, self.bad = {}, {}, set()
+
+
+def _with_ba(trace, engine, rng, extra=0.0, bad_every=None, spread=0.5):
+    """Drive the epoch's coins through Binary Agreement (hbbft_amd.binary_agreement): every
+    proposer with a coin runs a BA instance whose epochs 0 and 1 end with both values (estimate =
+    the fixed coins true, false) and whose epoch 2 flips the threshold coin of trace.coin_docs[p];
+    with probability ``extra`` the instance disagrees with that coin and runs on to epoch 5's
+    threshold coin (epochs 3, 4: both values; epoch 5: decides).  ``spread``: the fraction of the
+    message stream over which our SBV / Conf outcomes are released (the rest of the time our
+    instance lags the network, so early shares wait in its future-epoch queue)."""
+    keys = trace.keys
+    n, our = keys.n, 0
+    adv = getattr(trace, "adv", set())
+    others = [j for j in range(n) if j != our and j not in adv]
+    ba = BaTrace()
+    ps = sorted(trace.coin_docs)
+    h2 = [trace.hashes[p] for p in ps]
+    c2 = dict(zip(ps, hoststage.signature_parity(engine.g2_mul(h2, [keys.msk] * len(h2))))) if ps else {}
+    longer = [p for p in ps if rng.random() < extra]
+    docs5 = {p: coin_document(0, trace.hb_epoch, p, 5) for p in longer}
+    h5 = dict(zip(longer, hoststage.hash_g2([docs5[p] for p in longer]))) if longer else {}
+    c5 = dict(zip(longer, hoststage.signature_parity(engine.g2_mul([h5[p] for p in longer],
+                                                                       [keys.msk] * len(longer))))) if longer else {}
+    sh_keys, bases, scal = [], [], []
+    for p in ps:
+        ba.docs[(p, 2)] = trace.coin_docs[p]
+        if p in longer:
+            ba.sched[p] = [BOTH, BOTH, frozenset([not c2[p]]), BOTH, BOTH, frozenset([c5[p]])]
+            ba.decision[p], ba.coins[p] = c5[p], {2: c2[p], 5: c5[p]}
+            ba.docs[(p, 5)] = docs5[p]
+            for j in others:
+                forged = bad_every is not None and (p * n + j) % bad_every == 3
+                sh_keys.append((p, 5, j))
+                bases.append(h5[p])
+                scal.append(rng.randrange(1, R_ORDER) if forged else keys.sks[j])
+                if forged:
+                    ba.bad.add(("coin", p, j))
+        else:
+            ba.sched[p] = [BOTH, BOTH, frozenset([c2[p]])]
+            ba.decision[p], ba.coins[p] = c2[p], {2: c2[p]}
+        for j in others:
+            if (p, j) in trace.coin_shares:
+                ba.shares[(p, 2, j)] = trace.coin_shares[(p, j)]
+    if sh_keys:
+        ba.shares.update(zip(sh_keys, engine.g2_mul(bases, scal)))
+    ba.msgs = list(ba.shares)
+    rng.shuffle(ba.msgs)
+    span = max(1, int(spread * len(ba.msgs)))
+    for p in ps:
+        for e in range(len(ba.sched[p])):
+            a = rng.randrange(span)
+            ba.release[(p, e)] = (a, a + rng.randrange(max(1, span // 4)))
+    ba.bad |= {b for b in trace.bad if b[0] == "coin" and b[1] in ps}
+    ba.hashes = {(p, 2): trace.hashes[p] for p in ps}
+    ba.hashes.update({(p, 5): h5[p] for p in longer})
+    trace.ba = ba
+    return trace
+
+
+EpochTrace.with_ba = _with_ba
+
 
 class EpochResult:
     def __init__(self):
@@ -203,6 +278,9 @@ class EpochResult:
         self.checks_gpu = 0    # checks drained through the engine (incl. post-termination window tail)
         self.checks_consumed = 0  # verdicts the flows used (the reference's per-message checks)
         self.combines = 0
+        self.ba_decisions = {}  # proposer -> BA decision (BA-driven coins)
+        self.ba_coins = {}      # proposer -> {BA epoch: threshold coin}
+        self.ba_queued = 0      # coin shares that waited in a BA future-epoch queue
 
 
 def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelined=True, limit=None, decode=None):
@@ -265,7 +343,7 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
 
 
 def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True, slack=4, switch_interval=2e-4,
-              defer=True, raw=False):
+              defer=True, raw=False, ba=None):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
     ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
@@ -276,12 +354,17 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True
     when the instance asks; the reference's order, used to check the deferred path).
     ``raw``: the node receives bincode bytes (``trace.serialize()``): contributions are decoded in
     one batch (DeserializeCiphertext faults, epoch_state.rs:377-381) and every window of share
-    messages in one batch before it is queued (hbbft_amd.wire)."""
+    messages in one batch before it is queued (hbbft_amd.wire).
+    ``ba``: the coins come from Binary Agreement instances (``trace.with_ba``; default: when the
+    trace has a BA side) -- hbbft_amd.binary_agreement's epochs, fixed coins and future-epoch queue,
+    our SBV / Conf outcomes released along the message stream, coin combines deferred per window."""
+    if ba is None:
+        ba = getattr(trace, "ba", None) is not None
     old = sys.getswitchinterval()
     if pipelined and switch_interval:
         sys.setswitchinterval(switch_interval)
     try:
-        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw)
+        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba)
     finally:
         sys.setswitchinterval(old)
 
@@ -300,7 +383,7 @@ def _decoder(engine, raw_msgs, out, fn):
     return decode
 
 
-def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw):
+def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     ver = BatchVerifier(engine)
@@ -311,6 +394,118 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
 
     # --- Binary Agreement coins: ThresholdSign per BA instance that reaches a coin epoch
     t0 = time.perf_counter()
+    if ba:
+        coin_out = _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res)
+        coin_sh, dec_sh = ({}, {}) if raw else (trace.coin_shares, trace.dec_shares)
+        handed = {}
+        ni_sign = None
+        ts = {}
+        res.timing["coin_verify"] = time.perf_counter() - t0
+    else:
+        coin_out, handed, ni_sign, ts, coin_sh, dec_sh = _coins(engine, keys, trace, ver, window, our, threads,
+                                                               pipelined, limit, res, raw, sk, n, t0)
+    return _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n,
+                               t_all, coin_out, handed, ni_sign, ts, coin_sh, dec_sh)
+
+
+def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
+    """The BA-driven coin phase: one BinaryAgreementCoin per proposer with a coin (trace.ba).
+    Messages (p, e, j) come in windows; before a window's drain, every share of a running or
+    FUTURE epoch of its instance is queued (coin documents are hashed when first seen; a future
+    epoch's verdicts wait in the cache for the ThresholdSign its replay opens); between windows our
+    SBV / Conf outcomes whose release position has passed are fired, and the window's coin combines
+    run as one deferred batch whose results resume the BA state machines (which may replay queued
+    shares and complete further coins: repeated until no combine is pending).  Returns
+    {p: signature of the instance's first threshold coin}, as the synthetic phase does."""
+    ba = trace.ba
+    sk = keys.sks[our]
+    hb_id = 0
+    own_sig = {}
+    ni = NetworkInfo(our, range(keys.n), keys.t, keys.master_pk, keys.pks, sign_g2=lambda H: own_sig[bytes(H)])
+    # our own shares: one batched host signing for every coin document on the instances' paths
+    # (the reference signs each when its Conf round completes; the share is the same)
+    pe = sorted(ba.docs)
+    hs = [ver.doc_hash_of(ba.docs[k]) for k in pe]
+    hmap = dict(zip(pe, hs))
+    for h, sgn in zip(hs, hoststage.g2_mul(hs, [sk] * len(hs), threads=threads) if hs else []):
+        own_sig[bytes(h)] = sgn
+        ver.queue_sig(keys.pks[our], h, sgn)
+    bas = {p: BinaryAgreementCoin(ni, ver, (hb_id, trace.hb_epoch, p)) for p in sorted(ba.sched)}
+    fired = set()
+    queued_n = {}
+
+    def record(p, step):
+        res.faults += [("coin", p, f) for f in step.fault_log]
+        for d in step.output:
+            res.ba_decisions[p] = d
+
+    def local_events(pos):
+        progressed = True
+        while progressed:
+            progressed = False
+            for p, b in bas.items():
+                if b.decision is not None or b.pending is not None:
+                    continue
+                e = b.epoch
+                rel = ba.release.get((p, e))
+                if rel is None or e >= len(ba.sched[p]):
+                    continue
+                try:
+                    if b.conf_values is None and pos >= rel[0]:
+                        record(p, b.sbv_output(ba.sched[p][e]))
+                        progressed = True
+                    elif (b.conf_values is not None and not b.coin_decided and pos >= rel[1]
+                          and (p, e) not in fired):
+                        fired.add((p, e))
+                        record(p, b.conf_round_complete())
+                        progressed = True
+                except ProtocolError as err:
+                    res.errors.append(("coin", p, err))
+
+    def resolve():
+        while any(b.pending is not None for b in bas.values()):
+            ver.flush_combines()  # failures surface in resolve_pending as the reference's Err
+            for p, b in bas.items():
+                if b.pending is not None:
+                    try:
+                        record(p, b.resolve_pending())
+                    except ProtocolError as err:
+                        res.errors.append(("coin", p, err))
+
+    local_events(0)
+    resolve()
+    msgs = ba.msgs
+    for w0 in range(0, len(msgs), window):
+        batch = msgs[w0:w0 + window]
+        for p, e, j in batch:
+            b = bas[p]
+            if b.decision is None and e >= b.epoch and (b.epoch < e or not b.coin_decided):
+                c = queued_n.get((p, e), 0)
+                if limit is None or c < limit:
+                    ver.queue_sig(keys.pks[j], hmap[(p, e)], ba.shares[(p, e, j)])
+                    queued_n[(p, e)] = c + 1
+        ver.drain()
+        for p, e, j in batch:
+            try:
+                record(p, bas[p].handle_message(j, e, ba.shares[(p, e, j)]))
+            except ProtocolError as err:
+                res.errors.append(("coin", p, err))
+        resolve()
+        local_events(w0 + len(batch))
+        resolve()
+    local_events(len(msgs) + 1)
+    resolve()
+    out = {}
+    for p, b in bas.items():
+        res.ba_coins[p] = dict(b.coins)
+        res.ba_queued += b.queued
+        if 2 in b.signatures:
+            out[p] = b.signatures[2]
+    return out
+
+
+def _coins(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n, t0):
+    """The synthetic coin phase: one ThresholdSign per coin document (BA epoch 2), shares in windows."""
     ver.hash_docs([trace.coin_docs[p] for p in trace.coin_docs])
     own_sig = {}
     ni_sign = NetworkInfo(our, range(n), keys.t, keys.master_pk, keys.pks,
@@ -344,7 +539,11 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
                            _decoder(engine, trace.raw_coin, coin_sh, wire.decode_sig_share_msgs) if raw else None):
         coin_out[p] = out
     res.timing["coin_verify"] = time.perf_counter() - t0
+    return coin_out, handed, ni_sign, ts, coin_sh, dec_sh
 
+
+def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n, t_all,
+                        coin_out, handed, ni_sign, ts, coin_sh, dec_sh):
     # --- Subset output: the N ciphertexts into ThresholdDecrypt
     t0 = time.perf_counter()
     ps = sorted(trace.cts)

@@ -157,6 +157,14 @@ class BatchVerifier:
         h = self._docs.pop(doc, None)
         return h if h is not None else hoststage.hash_g2([doc])[0]
 
+    def doc_hash_of(self, doc):
+        """hash_g2(doc) from the hash_docs cache (kept for a later set_document), or hashed now."""
+        doc = bytes(doc)
+        h = self._docs.get(doc)
+        if h is None:
+            h = self._docs[doc] = hoststage.hash_g2([doc])[0]
+        return h
+
     # -------------------------------------------------------------- combines
     def combine_verify_g2(self, t, idx, shares, master_pk, h):
         """combine_and_verify_sig's crypto (src/threshold_sign.rs:249-270): (signature, status,

@@ -161,3 +161,35 @@ def test_epoch_random_adversary_raw_bytes(engine):
         assert flt.kind == want, (kind, p, flt)
     # every undecodable message is blamed whether or not its instance is still running
     assert {(k, p, x.node_id) for k, p, x in res.faults if x.kind == "DeserializeMessage"} == set(garbage)
+
+
+@pytest.mark.parametrize("n,extra", [(7, 0.5), (13, 0.3)])
+def test_epoch_coins_through_binary_agreement(engine, n, extra):
+    """The epoch's coins from Binary Agreement instances (hbbft_amd/binary_agreement.py) instead of a
+    synthetic coin set: epochs 0 and 1 end on both values, epoch 2 flips the threshold coin and
+    decides -- or, for a share of the instances, disagrees and runs on to epoch 5's coin.  Coin
+    shares of epochs the instance has not reached wait in its future-epoch queue
+    (binary_agreement.rs:245-266) and are replayed when it gets there (:489-519); coin combines are
+    deferred per window and resume the BA state machines.  Decisions and threshold coins equal the
+    schedule's (coins from msk * hash_g2(coin document), oracle parity); plaintexts equal the
+    proposals; only forged shares are blamed; window 1 unpipelined gives the same result."""
+    t = (n - 1) // 3
+    rng = random.Random(800 + n)
+    keys = NetworkKeys(engine, n, t, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=4, bad_every=9, proposal_bytes=60)
+    trace.with_ba(engine, rng, extra=extra, bad_every=9)
+    ba = trace.ba
+    assert any(len(s) > 3 for s in ba.sched.values())  # some instances need a second threshold coin
+    res = run_epoch(engine, keys, trace, window=16)
+    assert res.errors == []
+    assert res.plaintexts == trace.proposals
+    assert res.ba_decisions == ba.decision
+    assert res.ba_coins == ba.coins
+    assert res.ba_queued > 0
+    for p, sig in res.signatures.items():
+        assert sig == cbls.g2_mul(trace.hashes[p], keys.msk)
+        assert res.coins[p] == parity_oracle(sig) == ba.coins[p][2]
+    for kind, p, flt in res.faults:
+        assert (kind, p, flt.node_id) in (trace.bad | ba.bad), (kind, p, flt)
+    one = run_epoch(engine, keys, trace, window=1, pipelined=False)
+    assert (one.ba_decisions, one.ba_coins, one.plaintexts) == (res.ba_decisions, res.ba_coins, res.plaintexts)
