@@ -27,6 +27,7 @@ def coin_document(hb_id, hb_epoch, proposer_idx, ba_epoch):
     return struct.pack("<QQIQ", hb_id, hb_epoch, proposer_idx, ba_epoch)
 
 MAX_FUTURE_EPOCHS = 1000  # BinaryAgreement::new (binary_agreement.rs:214)
+REPLAY_SLACK = 4          # replayed coin shares verified beyond the t + 1 a coin needs
 
 
 class BinaryAgreementCoin:
@@ -86,7 +87,8 @@ class BinaryAgreementCoin:
         return self._handle_coin(sender, share)
 
     def _handle_coin(self, sender, share):  # :355-363
-        if self.coin_decided:
+        # a pending (deferred) coin's ThresholdSign has terminated: it ignores further shares
+        if self.coin_decided or self.pending is not None:
             return Step()
         try:
             ts_step = self.ts.handle_message(sender, share)
@@ -171,12 +173,23 @@ class BinaryAgreementCoin:
         replay = sorted(self.incoming.pop(self.epoch, {}).items())  # BTreeMap<sender, ..> order
         if replay and not self.coin_decided:
             # the replayed shares' checks in one drain (the reference verifies them one by one as
-            # handle_message_content reaches them; verdicts are pure, so the Steps are the same)
+            # handle_message_content reaches them; verdicts are pure, so the Steps are the same) --
+            # only as many as the coin can use: t + 1 + REPLAY_SLACK counting those a driver
+            # already pre-verified; a later share the coin still reads is verified on its own
+            # the coin reads the replay in sender order until t + 1 valid shares: verify that
+            # prefix (cached verdicts count; unknown ones are assumed valid) plus a small slack
+            need, have, queued = self.netinfo.num_faulty() + 1 + REPLAY_SLACK, 0, False
             for sender, share in replay:
                 pk = self.netinfo.public_key_share(sender)
-                if pk is not None:
+                if pk is None or have >= need:
+                    continue
+                v = self.verifier.cached_sig(pk, self.ts.doc_hash, share)
+                if v is None:
                     self.verifier.queue_sig(pk, self.ts.doc_hash, share)
-            self.verifier.drain()
+                    queued = True
+                have += 0 if v is False else 1
+            if queued:
+                self.verifier.drain()
         for sender, share in replay:
             step.extend(self._handle_coin(sender, share))
             if self.decision is not None:

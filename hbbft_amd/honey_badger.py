@@ -425,6 +425,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
     # our own shares: one batched host signing for every coin document on the instances' paths
     # (the reference signs each when its Conf round completes; the share is the same)
     pe = sorted(ba.docs)
+    ver.hash_docs([ba.docs[k] for k in pe])  # one threaded host-stage call for every coin document
     hs = [ver.doc_hash_of(ba.docs[k]) for k in pe]
     hmap = dict(zip(pe, hs))
     for h, sgn in zip(hs, hoststage.g2_mul(hs, [sk] * len(hs), threads=threads) if hs else []):
@@ -480,8 +481,11 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
         for p, e, j in batch:
             b = bas[p]
             if b.decision is None and e >= b.epoch and (b.epoch < e or not b.coin_decided):
+                # a current epoch's shares are read in arrival order: the first t + 1 + slack; a
+                # future epoch's are replayed in sender order (binary_agreement.rs:507-519), so
+                # all of them are pre-verified
                 c = queued_n.get((p, e), 0)
-                if limit is None or c < limit:
+                if limit is None or c < limit or e > b.epoch:
                     ver.queue_sig(keys.pks[j], hmap[(p, e)], ba.shares[(p, e, j)])
                     queued_n[(p, e)] = c + 1
         ver.drain()

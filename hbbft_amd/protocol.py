@@ -264,6 +264,10 @@ class BatchVerifier:
         if (bytes(pk), bytes(share)) not in self._sig.get(h, ()):
             self._qsig.append((bytes(pk), h, bytes(share)))
 
+    def cached_sig(self, pk, h, share):
+        """The cached verdict of a share check, or None (no engine call)."""
+        return self._sig.get(bytes(h), {}).get((bytes(pk), bytes(share)))
+
     def sig_valid(self, pk, h, share):
         self.lookups += 1
         h, k = bytes(h), (bytes(pk), bytes(share))
