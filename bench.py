@@ -240,6 +240,19 @@ def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_sim
     return e
 
 
+def reference_work(main_k, workcount):
+    """SURVEY §8(d)'s "reference work" beside the algorithmic roofline: the same verdicts as the
+    reference computes them (two separate pairings per check, workcount.REFERENCE_CHECK), priced
+    per unit at 300 MADs per Fp product, over the same measured launch time.  A throughput
+    equivalent, not a roofline: it counts work this kernel does not do."""
+    mad = workcount.mads(*workcount.REFERENCE_CHECK_OPS)
+    ach = main_k["units_per_launch"] * mad / (main_k["avg_launch_ms"] / 1e3) / 1e12 if main_k["avg_launch_ms"] else 0
+    return {"fp_ops_per_check": workcount.REFERENCE_CHECK, "mad_per_check": mad, "equivalent_T_mad_s": ach,
+            "equivalent_frac_of_peak": ach / MAD_PEAK_MEASURED,
+            "note": "two pairings per check as threshold_crypto's verify does (2 x (single-pair Miller + G2 walk + "
+                    "final exp)); the kernel's own count is roofline.mad_per_unit"}
+
+
 def pair_waves_per_simd(checks):
     """k_pair_verify: two lanes per check, 64-lane waves, 1,024 SIMDs."""
     w = checks * 2 / 64 / 1024
@@ -514,7 +527,7 @@ def main():
                        "streams": len(streams),
                        "documents_per_gpu": nh, "n_nodes": N_NODES, "f": F_FAULTY, "pairing_impl": args.impl,
                        "parallelism": "shard-by-batch x%d" % world},
-            "verdicts_ok": ok, "per_rank": per_rank,
+            "verdicts_ok": ok, "per_rank": per_rank, "reference_work": reference_work(main_k, workcount),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
                              traffic=pmc_traffic(KERNEL_NAMES[args.impl]), kernels=kernels,
                              note="achieved = checks x algorithmic MADs per check (workcount.PAIR_CHECK_WALK: "
@@ -655,6 +668,7 @@ def run_decrypt(args, eng, world, rank, dev):
             "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total, "streams": len(streams),
                        "ciphertexts": ncts, "parallelism": "shard-by-ciphertext x%d" % world},
             "verdicts_ok": ok, "combines_ok": out == want, "per_rank": per_rank,
+            "reference_work": reference_work(main_k, workcount),
             "combines_per_s_rank0": len(mine) / comb_s,                 # host-to-host, one call
             "combines_per_s_rank0_device": len(mine) / (comb_dev_ms / 1e3),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",

@@ -52,6 +52,12 @@ FINAL_EXP = EASY + HARD
 # is shared by the 64 shares of a document), one final exponentiation
 FP_MULS_PER_CHECK = MILLER_2PAIR + G2_WALK + FINAL_EXP
 
+# The reference's work for the same verdict (SURVEY §8(d) "reference work"): threshold_crypto's
+# verify_g2 computes e(pk_i, H) and e(g1, sig_i) as two separate pairings (pairing 0.14: each its own
+# G2Prepared walk, single-pair Miller loop and final exponentiation), then compares them.
+MILLER_1PAIR = NBITS * (F12_SQR + F12_MUL_014 + LINE_EVAL) + NADD * (F12_MUL_014 + LINE_EVAL)
+REFERENCE_CHECK = 2 * (MILLER_1PAIR + G2_WALK + FINAL_EXP)
+
 if __name__ == "__main__":
     print("miller", MILLER_2PAIR, "g2 walk", G2_WALK, "final exp", FINAL_EXP, "(easy", EASY, "hard", HARD,
           ") total", FP_MULS_PER_CHECK)
@@ -72,6 +78,7 @@ def mads(fpmul, fpsqr=0):
 PAIR_CHECK_WALK = (MILLER_2PAIR + G2_WALK + FINAL_EXP, FP_INV_SQR)   # k_pair_verify, one side walked
 PAIR_CHECK_TABLE = (MILLER_2PAIR + FINAL_EXP, FP_INV_SQR)            # k_pair_verify, both sides tabled
 PAIR_PREP_DOC = (G2_WALK, 0)                                         # k_pair_prep, per G2 point
+REFERENCE_CHECK_OPS = (REFERENCE_CHECK, FP_INV_SQR)                  # two separate pairings
 
 G1_DBL = (7, 5)
 G1_MADD = (11, 4)
