@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <mutex>
@@ -109,6 +110,12 @@ struct hbh_engine {
   bool fbtab_ready = false;  // fixed-base comb table of g1 (built on first use)
   // staging for host-pointer entry points
   DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
+  // split master check (hbh_combine_verify_g2): a second stream runs the partial Miller loops while
+  // the engine stream interpolates; partial Miller values in fval
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  DevBuf fval;
+  bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
 };
 
 namespace {
@@ -252,6 +259,7 @@ int hbh_engine_create(int device, hbh_engine** out) {
   HBH_CHECK(hipSetDevice(device));
   hbh_engine* e = new hbh_engine();
   e->device = device;
+  if (const char* v = std::getenv("HBH_SPLIT_CHECK")) e->split_check = std::atoi(v) != 0;
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
   if (err == hipSuccess) err = hipEventRecord(e->done, e->stream);
@@ -259,7 +267,11 @@ int hbh_engine_create(int device, hbh_engine** out) {
     err = hipEventCreateWithFlags(&e->slot_done[k], hipEventDisableTiming);
     if (err == hipSuccess) err = hipEventRecord(e->slot_done[k], e->stream);
   }
+  if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->fork, hipEventDisableTiming);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->join, hipEventDisableTiming);
   if (err != hipSuccess) {
+    if (e->side) (void)hipStreamDestroy(e->side);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return fail(HBH_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(err));
@@ -275,12 +287,16 @@ int hbh_engine_destroy(hbh_engine* e) {
   for (hipEvent_t ev : e->slot_done)
     if (ev) (void)hipEventSynchronize(ev);
   (void)hipStreamSynchronize(e->stream);
+  (void)hipStreamSynchronize(e->side);
   e->timer.clear();
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
-                    &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1]})
+                    &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval})
     b->release();
   (void)hipEventDestroy(e->done);
+  (void)hipEventDestroy(e->fork);
+  (void)hipEventDestroy(e->join);
+  (void)hipStreamDestroy(e->side);
   for (hipEvent_t ev : e->slot_done)
     if (ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
@@ -577,8 +593,9 @@ void host_div_x2(uint64_t q[4], uint64_t rem[2]) {
   rem[1] = r1;
 }
 
-void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* digits, int* status, bool g1 = false) {
-  constexpr uint64_t XA = 0xd201000000010000ull;
+// lambda_k(0) = prod_{j != k} x_j / (x_j - x_k) of every sample of each combine, canonical (4 x u64
+// LE per sample); status[c] = HBH_ERR_DUPLICATE_ENTRY and zero lambdas on a repeated x
+void host_lagrange(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* lam, int* status) {
   std::vector<HFr> x(m), num(m), den(m), pre(m);
   for (size_t c = 0; c < ncomb; c++) {
     const uint32_t* cx = xs + c * m;
@@ -596,9 +613,9 @@ void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* di
       den[k] = d;
     }
     status[c] = dup ? HBH_ERR_DUPLICATE_ENTRY : HBH_OK;
-    uint64_t* dg = digits + c * m * 4;
+    uint64_t* lc = lam + c * m * 4;
     if (dup) {
-      std::memset(dg, 0, m * 4 * sizeof(uint64_t));
+      std::memset(lc, 0, m * 4 * sizeof(uint64_t));
       continue;
     }
     pre[0] = den[0];
@@ -607,8 +624,19 @@ void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* di
     for (size_t k = m; k-- > 0;) {
       const HFr ik = k ? hfr_mul(inv, pre[k - 1]) : inv;
       if (k) inv = hfr_mul(inv, den[k]);
-      uint64_t q[4];
-      hfr_to_canon(hfr_mul(num[k], ik), q);
+      hfr_to_canon(hfr_mul(num[k], ik), lc + k * 4);
+    }
+  }
+}
+
+void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* digits, int* status, bool g1 = false) {
+  constexpr uint64_t XA = 0xd201000000010000ull;
+  host_lagrange(xs, ncomb, m, digits, status);  // in place: lambda_k's 4 words become its 4 digits
+  for (size_t c = 0; c < ncomb; c++) {
+    uint64_t* dg = digits + c * m * 4;
+    if (status[c] != HBH_OK) continue;
+    for (size_t k = 0; k < m; k++) {
+      uint64_t q[4] = {dg[k * 4], dg[k * 4 + 1], dg[k * 4 + 2], dg[k * 4 + 3]};
       if (g1) {  // lambda = d0 + d1 x^2
         uint64_t rem[2];
         host_div_x2(q, rem);
@@ -737,6 +765,105 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
   HBH_CHECK(hipStreamSynchronize(s));
   return HBH_OK;
 }
+
+// ThresholdSign::combine_and_verify_sig's master check split off the interpolation (few combines, the
+// latency case).  e(g1, sigma) == e(mpk, H) with sigma = sum_k lambda_k sigma_k is, by bilinearity,
+//   prod_k e(lambda_k g1, sigma_k) * e(-mpk, H) == 1,
+// which needs no sigma: its m + 1 Miller loops (two pairs per wave, k_wave's Miller-only mode) run on a
+// second stream WHILE the engine stream interpolates sigma, and one wave per combine multiplies the
+// partial values and runs the single final exponentiation (wave_prod_fe).  The verdict is the same
+// boolean for every input (an exact identity, no randomisation); lambda_k g1 comes from the host
+// comb (hbh__host_g1_gen_mul), computed while the GPU runs the interpolation.  A repeated index gives
+// zero lambdas (status DuplicateEntry), as in the interpolation.
+#ifndef HBH_SPLIT_CHECK_MAX
+#define HBH_SPLIT_CHECK_MAX 8
+#endif
+}  // namespace
+extern "C" int hbh__host_g1_gen_mul(size_t n, const uint8_t* scalars, uint8_t* out);
+extern "C" int hbh__host_g1_neg(const uint8_t* pk, uint8_t* neg_out);
+namespace {
+
+int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vector<uint32_t>& xs,
+                         const uint8_t* shares, const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out,
+                         int* status, uint8_t* verdicts) {
+  const size_t np = m + 1, nw = (np + 1) / 2, nchk = ncomb * nw, nq = ncomb * np;
+  std::vector<uint64_t> lam(ncomb * m * 4);
+  std::vector<int> lst(ncomb);
+  host_lagrange(xs.data(), ncomb, m, lam.data(), lst.data());
+  uint8_t negpk[HBH_G1_BYTES];
+  if (hbh__host_g1_neg(master_pk, negpk)) return fail(HBH_ERR_ARG, "master key coordinate >= p");
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  hipStream_t s = e->stream, s2 = e->side;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
+  // Q table: the shares, then one H per combine (the interpolation reads the shares' prefix)
+  HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
+  HBH_CHECK(e->in_b.ensure(nq * HBH_G2_BYTES));
+  HBH_CHECK(e->out_x.ensure(ncomb * HBH_G2_BYTES));
+  HBH_CHECK(e->status.ensure(ncomb * sizeof(int)));
+  HBH_CHECK(e->out_v.ensure(ncomb));
+  HBH_CHECK(e->in_p1.ensure(nchk * HBH_G1_BYTES));
+  HBH_CHECK(e->in_p2.ensure(nchk * HBH_G1_BYTES));
+  HBH_CHECK(e->in_i1.ensure(nchk * 4));
+  HBH_CHECK(e->in_i2.ensure(nchk * 4));
+  HBH_CHECK(e->fval.ensure(nchk * 144 * 4));
+  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xs.data(), ncomb * m * 4, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync(e->in_b.p, shares, ncomb * m * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemcpyAsync((uint8_t*)e->in_b.p + ncomb * m * HBH_G2_BYTES, hashes, ncomb * HBH_G2_BYTES,
+                           hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
+  HBH_CHECK(hipEventRecord(e->fork, s));
+  HBH_CHECK(hipStreamWaitEvent(s2, e->fork, 0));
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  int rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
+                             xs.data());
+  if (rc) return rc;
+  e->timer.end(s, tm);
+  // host, while the interpolation runs: lambda_k g1 and the two sides of every wave
+  std::vector<uint8_t> lg(ncomb * m * HBH_G1_BYTES);
+  if (hbh__host_g1_gen_mul(ncomb * m, (const uint8_t*)lam.data(), lg.data())) return fail(HBH_ERR_ARG, "g1 multiples");
+  std::vector<uint8_t> p0(nchk * HBH_G1_BYTES), p1(nchk * HBH_G1_BYTES, 0);
+  std::vector<uint32_t> i0(nchk), i1(nchk);
+  for (size_t c = 0; c < ncomb; c++)
+    for (size_t w = 0; w < nw; w++)
+      for (int sd = 0; sd < 2; sd++) {
+        const size_t k = 2 * w + sd, j = c * nw + w;
+        uint8_t* pd = (sd ? p1.data() : p0.data()) + j * HBH_G1_BYTES;
+        uint32_t* qi = sd ? &i1[j] : &i0[j];
+        if (k < m) {  // (lambda_k g1, sigma_k)
+          std::memcpy(pd, lg.data() + (c * m + k) * HBH_G1_BYTES, HBH_G1_BYTES);
+          *qi = (uint32_t)(c * m + k);
+        } else {  // (-mpk, H_c), then an inactive pad (P = O)
+          if (k == m) std::memcpy(pd, negpk, HBH_G1_BYTES);
+          else std::memset(pd, 0, HBH_G1_BYTES);
+          *qi = (uint32_t)(ncomb * m + c);
+        }
+      }
+  HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p0.data(), p0.size(), hipMemcpyHostToDevice, s2));
+  HBH_CHECK(hipMemcpyAsync(e->in_p2.p, p1.data(), p1.size(), hipMemcpyHostToDevice, s2));
+  HBH_CHECK(hipMemcpyAsync(e->in_i1.p, i0.data(), nchk * 4, hipMemcpyHostToDevice, s2));
+  HBH_CHECK(hipMemcpyAsync(e->in_i2.p, i1.data(), nchk * 4, hipMemcpyHostToDevice, s2));
+  hbl::PairSideDesc sd0 = {e->in_p1.p, e->in_b.p, nullptr, nullptr, (const uint32_t*)e->in_i1.p, nq};
+  hbl::PairSideDesc sd1 = {e->in_p2.p, e->in_b.p, nullptr, nullptr, (const uint32_t*)e->in_i2.p, nq};
+  hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
+  HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1, hbl::WAVE_MILLER_ONLY, nullptr, (uint32_t*)e->fval.p));
+  HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, (uint8_t*)e->out_v.p));
+  e->timer.end(s2, tp);
+  HBH_CHECK(hipEventRecord(e->join, s2));
+  HBH_CHECK(hipStreamWaitEvent(s, e->join, 0));
+  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * HBH_G2_BYTES, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, ncomb, hipMemcpyDeviceToHost, s));
+  {
+    const int rc_ = end_call(e, s);
+    if (rc_) return rc_;
+  }
+  HBH_CHECK(hipStreamSynchronize(s));
+  return HBH_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -774,6 +901,8 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
     if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
     xs[k] = idx[k] + 1;
   }
+  if (ncomb <= HBH_SPLIT_CHECK_MAX && e->split_check)
+    return combine_verify_split(e, ncomb, m, xs, shares, master_pk, hashes, out, status, verdicts);
   // P1 = master pk (one record per combine), P2 = the G1 generator (a flag, nothing uploaded)
   std::vector<uint8_t> p12(ncomb * HBH_G1_BYTES);
   for (size_t c = 0; c < ncomb; c++) std::memcpy(p12.data() + c * HBH_G1_BYTES, master_pk, HBH_G1_BYTES);

@@ -38,9 +38,11 @@ struct WaveSide {
 struct WaveArgs {
   int n;
   WaveSide s[2];
-  int flags;            // bit 0: negate P2; bit 1: conjugated value (single pairing)
+  int flags;            // bit 0: negate P2; bit 1: conjugated value (single pairing); bit 2: Miller only
   uint8_t* verdict;
   uint32_t* value_out;  // 144 canonical words per check (may be null)
+  const uint32_t* fin;  // product mode: nf Miller values (144 words, w-basis) per check; null otherwise
+  int nf;
 };
 
 // ---------------------------------------------------------------- LDS slots
@@ -372,11 +374,8 @@ HP_D const int4* wave_side(const WaveArgs& a, uint32_t* sm, int i, int h, int pa
   return tl;
 }
 
-__global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
-  extern __shared__ uint32_t sm[];
-  const int i = blockIdx.x;
-  if (i >= a.n) return;
-  const int lane = threadIdx.x, h = lane & 1, pair = lane >> 1;
+// the constant slots of tools/gen_wave_prog.py CONSTS and F = 1 (pair k writes slot k)
+HP_D void wave_consts(uint32_t* sm, int h, int pair) {
   switch (pair) {
     case 0: put_const(sm, h, 0, WV_ZW, WV_ZW); break;
     case 1: put_const(sm, h, 1, hb::ONE_L, WV_ZW); break;
@@ -400,19 +399,52 @@ __global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
       if (pair < 23) put_const(sm, h, hbw::WP_F + pair - 17, WV_ZW, WV_ZW);
       break;
   }
-  // the two sides: P (G1) -> XP, YP as Fp2 (x, 0); Q -> QX, QY and T = (Q, 1); activity flags
-  bool act0, act1, bad0, bad1;
-  const int4* tl0 = wave_side<0>(a, sm, i, h, pair, act0, bad0);
-  const int4* tl1 = wave_side<1>(a, sm, i, h, pair, act1, bad1);
-  const bool bad = bad0 || bad1;
-  if (bad) {  // index out of range: reject, never read past a table (uniform per workgroup)
-    if (lane == 0 && a.verdict) a.verdict[i] = 0;
-    return;
+}
+
+// Fp12 value k of check i (w-basis, 144 canonical words: component k at 24 k, lane h's half at
+// 12 h) into six consecutive slots from `slot` (pairs 0..5 load one component each)
+HP_D void wave_load12(uint32_t* sm, int h, int pair, int slot, const uint32_t* v) {
+  if (pair < 6) st_own(sm, slot + pair, h, fp_from_words(v + 24 * pair + 12 * h));
+}
+
+__global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
+  extern __shared__ uint32_t sm[];
+  const int i = blockIdx.x;
+  if (i >= a.n) return;
+  const int lane = threadIdx.x, h = lane & 1, pair = lane >> 1;
+  wave_consts(sm, h, pair);
+  if (a.fin) {
+    // product mode: F = prod_k fin[i][k] (one MULF program per factor), then the final
+    // exponentiation -- the second half of the split master check (hbh_combine_verify_g2)
+    const uint32_t* f = a.fin + (size_t)i * a.nf * 144;
+    wave_load12(sm, h, pair, hbw::WP_F, f);
+    for (int k = 1; k < a.nf; k++) {
+      wave_load12(sm, h, pair, hbw::WP_SIDE0, f + (size_t)k * 144);
+      __syncthreads();
+      run_stages(sm, hbw::WP_MULF_OFF, hbw::WP_MULF_N, h, pair, true, true, nullptr, nullptr);
+    }
+    __syncthreads();
+    run_stages(sm, hbw::WP_FE_OFF, hbw::WP_FE_N, h, pair, true, true, nullptr, nullptr);
+  } else {
+    // the two sides: P (G1) -> XP, YP as Fp2 (x, 0); Q -> QX, QY and T = (Q, 1); activity flags
+    bool act0, act1, bad0, bad1;
+    const int4* tl0 = wave_side<0>(a, sm, i, h, pair, act0, bad0);
+    const int4* tl1 = wave_side<1>(a, sm, i, h, pair, act1, bad1);
+    const bool bad = bad0 || bad1;
+    if (bad) {  // index out of range: reject, never read past a table (uniform per workgroup)
+      if (lane == 0 && a.verdict) a.verdict[i] = 0;
+      return;
+    }
+    __syncthreads();
+    const int mv = (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
+    run_stages(sm, hbw::WP_MILLER_OFF[mv], hbw::WP_MILLER_N[mv], h, pair, act0, act1, tl0, tl1);
+    if (a.flags & 4) {  // Miller only: f (w-basis) out, no final exponentiation
+      if (pair < 6 && a.value_out)
+        fp_to_words(ld_own(sm, hbw::WP_F + pair, h), a.value_out + (size_t)i * 144 + 24 * pair + 12 * h);
+      return;
+    }
+    run_stages(sm, hbw::WP_FE_OFF, hbw::WP_FE_N, h, pair, act0, act1, tl0, tl1);
   }
-  __syncthreads();
-  const int mv = (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
-  run_stages(sm, hbw::WP_MILLER_OFF[mv], hbw::WP_MILLER_N[mv], h, pair, act0, act1, tl0, tl1);
-  run_stages(sm, hbw::WP_FE_OFF, hbw::WP_FE_N, h, pair, act0, act1, tl0, tl1);
   // e = f^(3 (p^12 - 1) / r) in slots E0..E5 (w-basis)
   bool ok = true;
   if (pair < 6) {
@@ -452,6 +484,22 @@ hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairS
   a.flags = flags;
   a.verdict = verdict;
   a.value_out = value_out;
+  a.fin = nullptr;
+  a.nf = 0;
+  hipLaunchKernelGGL(hbs::k_wave, dim3((unsigned)n), dim3(64), wave_lds_bytes(), s, a);
+  return hipGetLastError();
+}
+
+hipError_t wave_prod_fe(hipStream_t s, int n, int nf, const uint32_t* fin, uint8_t* verdict) {
+  if (n <= 0) return hipSuccess;
+  if (nf <= 0 || !fin) return hipErrorInvalidValue;
+  hbs::WaveArgs a = {};
+  a.n = n;
+  a.flags = 0;
+  a.verdict = verdict;
+  a.value_out = nullptr;
+  a.fin = fin;
+  a.nf = nf;
   hipLaunchKernelGGL(hbs::k_wave, dim3((unsigned)n), dim3(64), wave_lds_bytes(), s, a);
   return hipGetLastError();
 }

@@ -38,6 +38,11 @@ hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairS
 size_t wave_lds_bytes();
 hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
                        uint8_t* verdict, uint32_t* value_out);
+// flags bit 2 (WAVE_MILLER_ONLY): wave_verify writes each check's Miller value f (144 canonical words,
+// w-basis) to value_out and stops there; wave_prod_fe then verifies prod_k fin[i][k] (nf values per
+// check) with one final exponentiation: verdict[i] = (FE(prod) == 1).
+constexpr int WAVE_MILLER_ONLY = 4;
+hipError_t wave_prod_fe(hipStream_t s, int n, int nf, const uint32_t* fin, uint8_t* verdict);
 
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).

@@ -133,6 +133,46 @@ def test_combine_verify_g2_matches_two_step(engine):
     assert out[0] == g2a(bytes.fromhex(doc["combined_uncompressed"]))
 
 
+@pytest.mark.parametrize("t", [0, 1, 21, 70])
+def test_combine_verify_split_matches_unsplit(engine, t):
+    """Up to 8 combines per call take the split master check (partial Miller loops of (lambda_k g1,
+    sigma_k) and (-mpk, H) beside the interpolation, one final exponentiation per combine); 9 and more
+    the interpolate-then-verify form.  Same signatures, statuses and verdicts on the same inputs:
+    valid, wrong document, a tampered share (random G2 point), a share at infinity, a duplicate index."""
+    rng = random.Random(700 + t)
+    coeffs = [rng.randrange(1, C.R) for _ in range(t + 1)]
+    mpk = cbls.g1_mul(G1, coeffs[0])
+    hs = [cbls.g2_mul(G2, rng.randrange(1, C.R)) for _ in range(2)]
+    n = max(t + 1, 8)
+    shares = [[cbls.g2_mul(h, tc.poly_eval(coeffs, i + 1)) for i in range(n)] for h in hs]
+    idx, pts, hashes = [], [], []
+    for c in range(9):
+        d = c % 2
+        sub = sorted(rng.sample(range(n), t + 1))
+        row = [shares[d][i] for i in sub]
+        h = hs[d]
+        if c == 2:
+            h = hs[1 - d]                      # wrong document
+        elif c == 3:
+            row[-1] = cbls.g2_mul(G2, rng.randrange(1, C.R))  # tampered share
+        elif c == 4:
+            row[0] = bytes(192)                # share at infinity
+        elif c == 5 and t > 0:
+            sub = [sub[0]] + sub[:t]           # duplicate index
+        idx.append(sub)
+        pts.append(row)
+        hashes.append(h)
+    out9, st9, v9 = engine.combine_verify_g2(t, idx, pts, mpk, hashes)
+    out8, st8, v8 = engine.combine_verify_g2(t, idx[:8], pts[:8], mpk, hashes[:8])
+    out1, st1, v1 = engine.combine_verify_g2(t, idx[:1], pts[:1], mpk, hashes[:1])
+    assert (out8, st8, v8) == (out9[:8], st9[:8], v9[:8])
+    assert (out1, st1, v1) == (out9[:1], st9[:1], v9[:1])
+    assert v9[0] == 1 and v9[1] == 1 and v9[2] == 0 and v9[3] == 0 and v9[4] == 0
+    assert [cbls.verify_g2(mpk, s, h) for s, h in zip(out9[:5], hashes[:5])] == [bool(x) for x in v9[:5]]
+    if t > 0:
+        assert st9[5] == 5 and v9[5] == 0
+
+
 def test_interpolate_edge_cases(engine):
     rng = random.Random(3)
     # t = 0 returns the sample itself

@@ -88,3 +88,26 @@ def test_inactive_pairs(progs):
     assert W.emulate(v, [(None, Q, False), (Pp, None, False)]) == ONE_W
     got = W.emulate(v, [(None, Q, False), (Pp, Q, False)], conj=True)
     assert got == tower_to_w(cube(C.pairing(Pp, Q)))
+
+
+def test_split_master_check(progs):
+    """The split master check of hbh_combine_verify_g2: partial Miller values of pairs (lambda_k g1,
+    sigma_k) and (-mpk, H), two pairs per wave (miller-only mode), multiplied by the MULF program and
+    one final exponentiation -- 1 exactly when the product of the pairings is 1."""
+    rnd = random.Random(5)
+    a = [rnd.randrange(1, C.R) for _ in range(3)]
+    b = [rnd.randrange(1, C.R) for _ in range(3)]
+    c = sum(x * y for x, y in zip(a, b)) % C.R
+    v = progs["variants"]["WW"]
+    P = [C.g1_mul(C.G1_GEN, x) for x in a]
+    Q = [C.g2_mul(C.G2_GEN, y) for y in b]
+    for cc, want in ((c, True), ((c + 1) % C.R, False)):
+        mpk = C.g1_mul(C.G1_GEN, cc)
+        fs = [W.emulate_miller(v, [(P[0], Q[0], False), (P[1], Q[1], False)]),
+              W.emulate_miller(v, [(P[2], Q[2], False), (mpk, C.G2_GEN, True)])]
+        assert (W.emulate_prod_fe(v, fs) == ONE_W) == want
+    # an inactive padding pair (P = O) contributes 1
+    mpk = C.g1_mul(C.G1_GEN, a[0] * b[0] % C.R)
+    f = W.emulate_miller(v, [(P[0], Q[0], False), (None, Q[1], False)])
+    g = W.emulate_miller(v, [(mpk, C.G2_GEN, True), (None, Q[2], False)])
+    assert W.emulate_prod_fe(v, [f, g]) == ONE_W

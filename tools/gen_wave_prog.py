@@ -37,6 +37,7 @@ SPECIAL_INV = 1
 # fixed slot map shared with the kernel prologue
 CONSTS = ["ZERO", "ONE"] + ["F1_%d" % k for k in range(6)] + ["F2_%d" % k for k in range(6)] + ["G1X", "G1Y", "G1NY"]
 SIDE_FIELDS = ["XP", "YP", "QX", "QY", "TX", "TY", "TZ"]
+MULF_G = ["S0_" + f for f in SIDE_FIELDS[:6]]
 
 
 class Prod:
@@ -380,6 +381,11 @@ class Builder:
         self.add(op_mul12(self.group("E"), A, X1))      # e = c w
         return self.group("E")
 
+    # ---- F <- F * G: the product of partial Miller values (the split master check of
+    # hbh_combine_verify_g2); G is loaded into side 0's first six slots, free once no Miller runs
+    def mulf(self):
+        self.add(op_mul12(self.F, self.F, MULF_G))
+
 
 # ------------------------------------------------------------------------------- scheduler
 class Stage:
@@ -654,12 +660,12 @@ def raw_lines(Q):
     return out
 
 
-def emulate(prog, sides, conj=False):
-    """Run `prog` (dict from build()) for one check.  sides[k] = (Pk, Qk, negate): Pk affine G1
-    (x, y) or None or 'GEN'; Qk affine G2 ((x0, x1), (y0, y1)) or None.  Returns f as 6 Fp2 (w-basis)
-    after the program, conjugated when `conj`."""
+PROD_BASE = Builder("fixed").slots["PROD0"]  # fixed slots: the same index in every program
+
+
+def _setup(prog, sides):
+    """LDS image, pair activity and table lines of one check before its Miller program."""
     S = prog["slots"]
-    inv = {v: k for k, v in S.items()}
     mem = [(0, 0)] * 256
     for k, v in const_values().items():
         mem[S[k]] = v
@@ -686,75 +692,107 @@ def emulate(prog, sides, conj=False):
         mem[S["S%d_TZ" % k]] = (1, 0)
         act.append(not pinf and Qk is not None)
         tables.append(raw_lines(Qk))
+    return mem, act, tables
 
-    def run(hdrs, pdesc, adesc):
-        nonlocal mem
-        for st in range(len(hdrs) // 4):
-            h0, po, ao, h3 = hdrs[4 * st:4 * st + 4]
-            kind, j1, j2 = h0 & 3, (h0 >> 2) & 7, (h0 >> 5) & 7
-            special = (h0 >> 12) & 0xF
-            npairs, nouts = (h0 >> 16) & 63, (h0 >> 22) & 63
-            K = 2 if kind == 1 else 1
-            new = {}
-            if special == SPECIAL_INV:
-                new[(h3 >> 8) & 0xFF] = f2inv(mem[h3 & 0xFF])
-            prod = {}
-            for j in range(npairs):
-                acc = (0, 0)
-                for t in range(K):
-                    w = pdesc[po + j * K + t]
 
-                    def operand(base, other, sc, negb, conjb):
-                        v = mem[base]
-                        s = {0: 0, 1: 1, 2: -1}[sc]
-                        if s:
-                            v = f2add(v, f2scale(mem[other], s))
-                        if negb:
-                            v = f2scale(v, -1)
-                        if conjb:
-                            v = f2conj(v)
-                        return v
+def _run(mem, act, tables, hdrs, pdesc, adesc, names=None):
+    """Execute the stages of one program on the LDS image `mem` (exact Fp2 arithmetic)."""
+    for st in range(len(hdrs) // 4):
+        h0, po, ao, h3 = hdrs[4 * st:4 * st + 4]
+        kind, j1, j2 = h0 & 3, (h0 >> 2) & 7, (h0 >> 5) & 7
+        special = (h0 >> 12) & 0xF
+        npairs, nouts = (h0 >> 16) & 63, (h0 >> 22) & 63
+        K = 2 if kind == 1 else 1
+        new = {}
+        if special == SPECIAL_INV:
+            new[(h3 >> 8) & 0xFF] = f2inv(mem[h3 & 0xFF])
+        prod = {}
+        for j in range(npairs):
+            acc = (0, 0)
+            for t in range(K):
+                w = pdesc[po + j * K + t]
 
-                    X = operand(w & 0xFF, (w >> 8) & 0xFF, (w >> 32) & 3, (w >> 36) & 1, (w >> 37) & 1)
-                    Y = operand((w >> 16) & 0xFF, (w >> 24) & 0xFF, (w >> 34) & 3, (w >> 38) & 1, (w >> 39) & 1)
-                    acc = f2add(acc, f2mul(X, X) if kind == 2 else f2mul(X, Y))
-                prod[S["PROD%d" % j]] = acc
-            view = lambda i: prod[i] if i in prod else mem[i]
-            for o in range(nouts):
-                ws = adesc[(ao + o) * 8:(ao + o) * 8 + 8]
-                dst, gate, defone = ws[0] & 0xFF, (ws[0] >> 8) & 3, (ws[0] >> 10) & 1
-                accp, acct = (0, 0), (0, 0)
-                for t in range(j1 + j2):
-                    tm = ws[1 + t]
-                    src, c, cj = tm & 0xFF, (tm >> 8) & 0xF, (tm >> 12) & 1
-                    c = c - 16 if c >= 8 else c
-                    v = view(src)
-                    if cj:
+                def operand(base, other, sc, negb, conjb):
+                    v = mem[base]
+                    s = {0: 0, 1: 1, 2: -1}[sc]
+                    if s:
+                        v = f2add(v, f2scale(mem[other], s))
+                    if negb:
+                        v = f2scale(v, -1)
+                    if conjb:
                         v = f2conj(v)
-                    if t < j1:
-                        accp = f2add(accp, f2scale(v, c))
-                    else:
-                        acct = f2add(acct, f2scale(v, c))
-                val = f2add(accp, f2xi(acct))
-                if gate and not act[gate - 1]:
-                    val = (1, 0) if defone else (0, 0)
-                assert dst not in new, (st, inv.get(dst))
-                new[dst] = val
-            for side in (0, 1):
-                e = (h3 >> (16 * side)) & 0xFFFF
-                if e & 1 and special == 0:
-                    step, base = (e >> 1) & 0x7F, e >> 8
-                    for c in range(3):
-                        new[base + c] = tables[side][step][c]
-            for k, v in new.items():
-                mem[k] = v
+                    return v
 
-    run(*prog["miller"])
-    run(*prog["fe"])
+                X = operand(w & 0xFF, (w >> 8) & 0xFF, (w >> 32) & 3, (w >> 36) & 1, (w >> 37) & 1)
+                Y = operand((w >> 16) & 0xFF, (w >> 24) & 0xFF, (w >> 34) & 3, (w >> 38) & 1, (w >> 39) & 1)
+                acc = f2add(acc, f2mul(X, X) if kind == 2 else f2mul(X, Y))
+            prod[PROD_BASE + j] = acc
+        view = lambda i: prod[i] if i in prod else mem[i]
+        for o in range(nouts):
+            ws = adesc[(ao + o) * 8:(ao + o) * 8 + 8]
+            dst, gate, defone = ws[0] & 0xFF, (ws[0] >> 8) & 3, (ws[0] >> 10) & 1
+            accp, acct = (0, 0), (0, 0)
+            for t in range(j1 + j2):
+                tm = ws[1 + t]
+                src, c, cj = tm & 0xFF, (tm >> 8) & 0xF, (tm >> 12) & 1
+                c = c - 16 if c >= 8 else c
+                v = view(src)
+                if cj:
+                    v = f2conj(v)
+                if t < j1:
+                    accp = f2add(accp, f2scale(v, c))
+                else:
+                    acct = f2add(acct, f2scale(v, c))
+            val = f2add(accp, f2xi(acct))
+            if gate and not act[gate - 1]:
+                val = (1, 0) if defone else (0, 0)
+            assert dst not in new, (st, dst)
+            new[dst] = val
+        for side in (0, 1):
+            e = (h3 >> (16 * side)) & 0xFFFF
+            if e & 1 and special == 0:
+                step, base = (e >> 1) & 0x7F, e >> 8
+                for c in range(3):
+                    new[base + c] = tables[side][step][c]
+        for k, v in new.items():
+            mem[k] = v
+
+
+def emulate(prog, sides, conj=False):
+    """Run `prog` (dict from build()) for one check.  sides[k] = (Pk, Qk, negate): Pk affine G1
+    (x, y) or None or 'GEN'; Qk affine G2 ((x0, x1), (y0, y1)) or None.  Returns f as 6 Fp2 (w-basis)
+    after the program, conjugated when `conj`."""
+    mem, act, tables = _setup(prog, sides)
+    _run(mem, act, tables, *prog["miller"])
+    _run(mem, act, tables, *prog["fe"])
     f = [mem[prog["slots_fe"]["E%d" % k]] for k in range(6)]
     if conj:
         f = [f[k] if k % 2 == 0 else f2scale(f[k], -1) for k in range(6)]
     return f
+
+
+def emulate_miller(prog, sides):
+    """The Miller program alone (k_wave's miller-only mode): f as 6 Fp2 (w-basis)."""
+    mem, act, tables = _setup(prog, sides)
+    _run(mem, act, tables, *prog["miller"])
+    return [mem[prog["slots"]["F%d" % k]] for k in range(6)]
+
+
+def emulate_prod_fe(prog, fs):
+    """k_wave's product mode: F = fs[0] * fs[1] * ... (one MULF program per factor), then the final
+    exponentiation; returns e (w-basis)."""
+    S = prog["slots"]
+    mem = [(0, 0)] * 256
+    for k, v in const_values().items():
+        mem[S[k]] = v
+    for k in range(6):
+        mem[S["F%d" % k]] = fs[0][k]
+    for f in fs[1:]:
+        for k in range(6):
+            mem[S[MULF_G[k]]] = f[k]
+        _run(mem, [True, True], [None, None], *prog["mulf"])
+    _run(mem, [True, True], [None, None], *prog["fe"])
+    return [mem[prog["slots_fe"]["E%d" % k]] for k in range(6)]
 
 
 # ------------------------------------------------------------------------------- build / emit
@@ -823,6 +861,15 @@ def build():
         out["variants"][m] = {"miller": encode(b, st), "fe": fe_enc, "slots": b.slots, "slots_fe": fe.slots,
                               "nstages_miller": len(st), "nstages_fe": len(fe_stages),
                               "stages_miller": st, "stages_fe": fe_stages}
+    mf = Builder("mulf")
+    mf.mulf()
+    mf_stages = schedule(mf.ops)
+    mf.slots = allocate(mf, mf_stages)
+    mf_enc = encode(mf, mf_stages)
+    for v in out["variants"].values():
+        v["mulf"] = mf_enc
+    out["mulf"] = mf_enc
+    out["nstages_mulf"] = len(mf_stages)
     out["nslots"] = nslots
     out["slots"] = fe.slots
     return out
@@ -857,10 +904,13 @@ def emit(out, path):
         return h0, len(h) // 4
 
     fe_off, fe_n = append(fe)
+    mf_off, mf_n = append(out["mulf"])
     for m in MODES:
         mo, mn = append(out["variants"][m]["miller"])
         info.append((mo, mn))
     lines.append("constexpr int WP_FE_OFF = %d, WP_FE_N = %d;" % (fe_off, fe_n))
+    lines.append("// F <- F * G with G in side 0's slots XP YP QX QY TX TY (product of partial Miller values)")
+    lines.append("constexpr int WP_MULF_OFF = %d, WP_MULF_N = %d;" % (mf_off, mf_n))
     lines.append("// Miller programs: WALK/TABLE for side 0 and side 1 -> index (side0 is TABLE) * 2 + (side1 is TABLE)")
     lines.append("constexpr int WP_MILLER_OFF[4] = {%s};" % ", ".join(str(i[0]) for i in info))
     lines.append("constexpr int WP_MILLER_N[4] = {%s};" % ", ".join(str(i[1]) for i in info))
