@@ -217,6 +217,71 @@ HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, boo
   st_own(sm, ws[0] & 0xFF, h, r);
 }
 
+// ---------------------------------------------------------------- CYC runs (register-resident squarings)
+// Granger-Scott squaring splits into three Fp4 squarings: (f0, f3) -> (r0, r3), (f1, f4) -> (r2, r5),
+// (f2, f5) -> (r1, r4), each of three Fp2 squares sA = A^2, sB = B^2, sAB = (A + B)^2 and outputs
+//   X = 3 (sA + xi sB) - 2 L,  Y = 3 (sAB - sA - sB) + 2 L,  Z = 3 xi (sAB - sA - sB) + 2 L
+// with L the input at the output's position.  Lane row g (16 lanes) runs one Fp4 squaring: pairs 0 / 1
+// hold A / B (own Fp2 component), pair 2 squares A + B; the squares and the two inputs move by lane
+// shuffles (ds_bpermute) inside the wave -- no LDS slot traffic and no barrier per squaring.  Row 0
+// keeps (f0, f3).  Rows 1 and 2 swap roles each squaring: the row squaring (f1, f4) produces the next
+// (f2, f5) and vice versa, so squaring inputs never move; only L crosses between rows 1 and 2.
+HP_D Fp shfl_fp(const Fp& a, int src_lane) {
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.l[i] = __builtin_amdgcn_ds_bpermute(src_lane << 2, a.l[i]);
+  return r;
+}
+// reduce(3 t + k a) for k = +-2 chosen at run time (fp_red_mk's one-pass reduction, same bounds)
+HP_D Fp fp_red_3k(const Fp& t, const Fp& a, int k) {
+  const int64_t top = (int64_t)t.l[NL - 1] * 3 + (int64_t)k * a.l[NL - 1];
+  const int32_t q = (int32_t)((top * QINV) >> 32);
+  Fp r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    acc += (int64_t)t.l[i] * 3 + (int64_t)k * a.l[i] - (int64_t)q * (int32_t)P_L[i];
+    r.l[i] = (int32_t)acc & MASK28;
+    acc >>= 28;
+  }
+  r.l[NL - 1] = (int32_t)(acc + top - (int64_t)q * (int32_t)P_L[NL - 1]);
+  return r;
+}
+// position of the value a holder lane keeps: role 0 holds (f0, f3), role 1 (f1, f4), role 2 (f2, f5)
+HP_D int cyc_pos(int role, int j) { return role + 3 * j; }
+
+// w0 = six source slots (a byte each, w-basis order); w1 = six destination slots | count << 48 |
+// conjugate-the-result << 56
+HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
+  const int h = lane & 1, row = lane >> 4, j = (lane >> 1) & 7;
+  const bool holder = row < 3 && j < 2;
+  const int count = (int)((w1 >> 48) & 0xFF);
+  const bool conj = ((w1 >> 56) & 1) != 0;
+  int role = row < 3 ? row : 0;
+  Fp v = fp_zero();
+  if (holder) v = ld_own(sm, (int)((w0 >> (8 * cyc_pos(role, j))) & 0xFF), h);
+  const int base = (lane & 0x30) | h;  // this row's pair 0, own component
+  const int partner = (row == 1 || row == 2) ? (((3 - row) << 4) | (lane & 15)) : lane;
+#pragma unroll 1
+  for (int it = 0; it < count; it++) {
+    const Fp A = shfl_fp(v, base), B = shfl_fp(v, base + 2);
+    const Fp x = j == 2 ? fp_add(A, B) : v;
+    const Fp sq = h_sqr(x);
+    const Fp sA = shfl_fp(sq, base), sB = shfl_fp(sq, base + 2), sAB = shfl_fp(sq, base + 4);
+    const Fp L = shfl_fp(v, partner);
+    // role 0 / 1: pair 0 -> X (r0 / r2), pair 1 -> Y (r3 / r5); role 2: pair 0 -> Z (r1), pair 1 -> X (r4)
+    const bool isX = role != 2 ? j == 0 : j == 1;
+    const bool isZ = role == 2 && j == 0;
+    const Fp u = fp_sub2l(sAB, sA, sB);
+    const Fp T = isX ? h_add_xi_l(sA, sB) : (isZ ? h_xi_l(u) : u);
+    Fp r = fp_red_3k(T, L, isX ? -2 : 2);
+    if (conj && it == count - 1 && (role == 2 ? j == 0 : j == 1)) r = fp_neg(r);  // odd positions
+    v = r;
+    if (row == 1 || row == 2) role = 3 - role;  // (f1, f4) <-> (f2, f5)
+  }
+  if (holder) st_own(sm, (int)((w1 >> (8 * cyc_pos(role, j))) & 0xFF), h, v);
+}
+
 // this lane's descriptors of one stage (product: K u64 of its pair; assembly: 8 u16 of its output)
 struct StageDesc {
   uint4 hd;
@@ -230,7 +295,10 @@ HP_D StageDesc load_stage(const uint4* hdr, int st, int pair) {
   const int kind = fl & 3, npairs = (fl >> 16) & 63, nouts = (fl >> 22) & 63;
   d.p0 = d.p1 = 0;
   d.ad = make_uint4(0, 0, 0, 0);
-  if (kind != 3 && pair < npairs) {
+  if (((fl >> 12) & 0xF) == 2) {  // CYC run: source and destination slots, count, conjugation
+    d.p0 = hbw::WP_PDESC[d.hd.y];
+    d.p1 = hbw::WP_PDESC[d.hd.y + 1];
+  } else if (kind != 3 && pair < npairs) {
     if (kind == 1) {
       d.p0 = hbw::WP_PDESC[d.hd.y + 2 * pair];
       d.p1 = hbw::WP_PDESC[d.hd.y + 2 * pair + 1];
@@ -267,7 +335,9 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
         tslot = (int)(e >> 8);
       }
     }
-    if (special == 1) {
+    if (special == 2) {
+      cyc_run(sm, 2 * pair + h, cur.p0, cur.p1);
+    } else if (special == 1) {
 #ifdef WV_SKIP_INV  // timing experiment only: wrong verdicts
       if (false) {
 #else

@@ -33,6 +33,7 @@ COEF_LIMIT = 8  # per accumulator: sum of positive / of negative coefficients (i
 
 KIND = {"M1": 0, "M2": 1, "SQ": 2, "NONE": 3}
 SPECIAL_INV = 1
+SPECIAL_CYC = 2  # a run of cyclotomic squarings kept in registers (k_wave.hip cyc_run)
 
 # fixed slot map shared with the kernel prologue
 CONSTS = ["ZERO", "ONE"] + ["F1_%d" % k for k in range(6)] + ["F2_%d" % k for k in range(6)] + ["G1X", "G1Y", "G1NY"]
@@ -76,7 +77,10 @@ class Op:
                     if s is not None:
                         r.add(s)
         if self.special:
-            r.add(self.special[1])
+            if self.special[0] == "CYC":
+                r |= set(self.special[1])
+            else:
+                r.add(self.special[1])
         return r
 
     def reads_asm(self):
@@ -91,7 +95,10 @@ class Op:
     def writes(self):
         w = {o.dst for o in self.outs}
         if self.special:
-            w.add(self.special[2])
+            if self.special[0] == "CYC":
+                w |= set(self.special[2])
+            else:
+                w.add(self.special[2])
         if self.tload:
             w |= set(self.tload[3])
         return w
@@ -200,6 +207,14 @@ def op_cyclo(dst, f, conj_out=False):
     return Op("SQ", prods, outs, name="cyclo")
 
 
+def op_cycrun(dst, f, count, conj_out=False):
+    """`count` Granger-Scott cyclotomic squarings of f (op_cyclo's formulas) in ONE stage: k_wave's
+    cyc_run keeps the three Fp4 squarings in registers of three lane rows and exchanges values by DPP
+    and lane shuffles -- no LDS round trip or barrier per squaring.  dst conjugated when conj_out."""
+    assert 1 <= count <= 255
+    return Op("CYC", special=("CYC", list(f), list(dst), count, bool(conj_out)), name="cycrun")
+
+
 def op_frob1(dst, f):
     prods = [[Prod(f[k], "F1_%d" % k, conjx=True)] for k in range(6)]
     return Op("M1", prods, [Out(dst[k], [(P_(k), 1, 0)]) for k in range(6)], name="frob1")
@@ -217,8 +232,9 @@ def op_copy(dst, src, conj_out=False):
 
 # ------------------------------------------------------------------------------- programs
 class Builder:
-    def __init__(self, name):
+    def __init__(self, name, cyc_runs=True):
         self.name = name
+        self.cyc_runs = cyc_runs  # final exponentiation squarings as CYC runs (False: one SQ stage each)
         self.slots = {}
         for c in CONSTS:
             self.slot(c)
@@ -357,16 +373,25 @@ class Builder:
 
         def exp(dst, base, plus1, conj_out):
             e = X_ABS + (1 if plus1 else 0)
-            ops = []
-            first = True
+            src, run = base, 0
             for k in range(62, -1, -1):
-                last_sq = (k == 0 and not ((e >> k) & 1))
-                ops.append(self.add(op_cyclo(dst, base if first else dst, conj_out=conj_out and last_sq)))
-                first = False
-                if (e >> k) & 1:
-                    ops.append(self.add(op_mul12(dst, dst, base, conj_out=conj_out and k == 0)))
+                run += 1
+                bit = (e >> k) & 1
+                if bit or k == 0:  # a run of squarings ends at each set bit (and at the end)
+                    if self.cyc_runs:
+                        self.add(op_cycrun(dst, src, run, conj_out=conj_out and k == 0 and not bit))
+                    else:
+                        for q in range(run):
+                            last = q == run - 1 and k == 0 and not bit
+                            self.add(op_cyclo(dst, src if q == 0 else dst, conj_out=conj_out and last))
+                    src, run = dst, 0
+                if bit:
+                    self.add(op_mul12(dst, dst, base, conj_out=conj_out and k == 0))
 
-        self.add(op_cyclo(X1, G))                       # cyclo(g) g, needed for w
+        if self.cyc_runs:
+            self.add(op_cycrun(X1, G, 1))               # cyclo(g) g, needed for w
+        else:
+            self.add(op_cyclo(X1, G))
         self.add(op_mul12(X1, X1, G))
         exp(T, G, True, True)                           # t = g^(x-1)
         exp(A, T, True, True)                           # a = t^(x-1)
@@ -403,7 +428,7 @@ class Stage:
 def op_ok_in(op, st):
     if op.kind == "TLOAD":
         return op.tload[0] not in st.tload and st.special is None
-    if op.kind == "INV":
+    if op.kind in ("INV", "CYC"):
         return not st.ops
     if st.special is not None:
         return False
@@ -447,7 +472,7 @@ def schedule(ops):
         st.ops.append(op)
         if op.kind == "TLOAD":
             st.tload[op.tload[0]] = op
-        elif op.kind == "INV":
+        elif op.kind in ("INV", "CYC"):
             st.special = op
             st.kind = "NONE"
         else:
@@ -554,7 +579,16 @@ def encode(b, stages):
         h0 = KIND[st.kind] | (st.j1 << 2) | (st.j2 << 5) | (flags_xsum << 8) | (flags_ysum << 9) | (flags_neg << 10)
         h0 |= (flags_conj << 11)
         h3 = 0
-        if st.special is not None:
+        if st.special is not None and st.special.special[0] == "CYC":
+            _, src, dst, count, conj = st.special.special
+            w0 = sum(S[n] << (8 * k) for k, n in enumerate(src))
+            w1 = sum(S[n] << (8 * k) for k, n in enumerate(dst)) | (count << 48) | (int(conj) << 56)
+            key = (w0, w1)
+            if key not in pcache:
+                pcache[key] = len(pdesc)
+                pdesc.extend([w0, w1])
+            h0 |= SPECIAL_CYC << 12
+        elif st.special is not None:
             h0 |= SPECIAL_INV << 12
             h3 = S[st.special.special[1]] | (S[st.special.special[2]] << 8)
         else:
@@ -586,6 +620,19 @@ def f2conj(a):
 
 def f2xi(a):
     return ((a[0] - a[1]) % P, (a[0] + a[1]) % P)
+
+
+def cyclo_w(f):
+    """Granger-Scott cyclotomic squaring on the w-basis (op_cyclo's formulas)."""
+    sq = lambda x: f2mul(x, x)
+    s0, s3, s03 = sq(f[0]), sq(f[3]), sq(f2add(f[0], f[3]))
+    s1, s4, s14 = sq(f[1]), sq(f[4]), sq(f2add(f[1], f[4]))
+    s2, s5, s25 = sq(f[2]), sq(f[5]), sq(f2add(f[2], f[5]))
+    lin = lambda a, b, c: f2add(f2scale(a, 3), f2scale(b, c))
+    u = lambda sab, sa, sb: f2add(sab, f2scale(f2add(sa, sb), -1))
+    return [lin(f2add(s0, f2xi(s3)), f[0], -2), f2add(f2scale(f[1], 2), f2scale(f2xi(u(s25, s2, s5)), 3)),
+            lin(f2add(s1, f2xi(s4)), f[2], -2), lin(u(s03, s0, s3), f[3], 2),
+            lin(f2add(s2, f2xi(s5)), f[4], -2), lin(u(s14, s1, s4), f[5], 2)]
 
 
 def f2pow(a, e):
@@ -704,6 +751,16 @@ def _run(mem, act, tables, hdrs, pdesc, adesc, names=None):
         npairs, nouts = (h0 >> 16) & 63, (h0 >> 22) & 63
         K = 2 if kind == 1 else 1
         new = {}
+        if special == SPECIAL_CYC:
+            w0, w1 = pdesc[po], pdesc[po + 1]
+            f = [mem[(w0 >> (8 * k)) & 0xFF] for k in range(6)]
+            for _ in range((w1 >> 48) & 0xFF):
+                f = cyclo_w(f)
+            if (w1 >> 56) & 1:
+                f = [f[k] if k % 2 == 0 else f2scale(f[k], -1) for k in range(6)]
+            for k in range(6):
+                mem[(w1 >> (8 * k)) & 0xFF] = f[k]
+            continue
         if special == SPECIAL_INV:
             new[(h3 >> 8) & 0xFF] = f2inv(mem[h3 & 0xFF])
         prod = {}
