@@ -772,14 +772,14 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
 // which needs no sigma: its m + 1 Miller loops (two pairs per wave, k_wave's Miller-only mode) run on a
 // second stream WHILE the engine stream interpolates sigma, and one wave per combine multiplies the
 // partial values and runs the single final exponentiation (wave_prod_fe).  The verdict is the same
-// boolean for every input (an exact identity, no randomisation); lambda_k g1 comes from the host
-// comb (hbh__host_g1_gen_mul), computed while the GPU runs the interpolation.  A repeated index gives
-// zero lambdas (status DuplicateEntry), as in the interpolation.
+// boolean for every input (an exact identity, no randomisation); lambda_k g1 comes from the device comb
+// table summed in a 5-level tree on lane quads (k_g1_gen_quad) on the side stream, left in Jacobian
+// form: the Miller kernel scales each line by Z^3 instead of inverting Z (WAVE_JAC_P).  A repeated index gives zero
+// lambdas (status DuplicateEntry), as in the interpolation.
 #ifndef HBH_SPLIT_CHECK_MAX
 #define HBH_SPLIT_CHECK_MAX 8
 #endif
 }  // namespace
-extern "C" int hbh__host_g1_gen_mul(size_t n, const uint8_t* scalars, uint8_t* out);
 extern "C" int hbh__host_g1_neg(const uint8_t* pk, uint8_t* neg_out);
 namespace {
 
@@ -805,8 +805,8 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   HBH_CHECK(e->out_x.ensure(ncomb * HBH_G2_BYTES));
   HBH_CHECK(e->status.ensure(ncomb * sizeof(int)));
   HBH_CHECK(e->out_v.ensure(ncomb));
-  HBH_CHECK(e->in_p1.ensure(nchk * HBH_G1_BYTES));
-  HBH_CHECK(e->in_p2.ensure(nchk * HBH_G1_BYTES));
+  HBH_CHECK(e->in_p1.ensure(nchk * 3 * 48));
+  HBH_CHECK(e->in_p2.ensure(nchk * 3 * 48));
   HBH_CHECK(e->in_i1.ensure(nchk * 4));
   HBH_CHECK(e->in_i2.ensure(nchk * 4));
   HBH_CHECK(e->fval.ensure(nchk * 144 * 4));
@@ -817,41 +817,52 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
   HBH_CHECK(hipEventRecord(e->fork, s));
   HBH_CHECK(hipStreamWaitEvent(s2, e->fork, 0));
-  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  int rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
-                             xs.data());
-  if (rc) return rc;
-  e->timer.end(s, tm);
-  // host, while the interpolation runs: lambda_k g1 and the two sides of every wave
-  std::vector<uint8_t> lg(ncomb * m * HBH_G1_BYTES);
-  if (hbh__host_g1_gen_mul(ncomb * m, (const uint8_t*)lam.data(), lg.data())) return fail(HBH_ERR_ARG, "g1 multiples");
-  std::vector<uint8_t> p0(nchk * HBH_G1_BYTES), p1(nchk * HBH_G1_BYTES, 0);
+  // the two sides of every wave: (-mpk, H_c) and the inactive pad (P = O) from the host, lambda_k g1
+  // written over the zero entries by k_g1_gen_tree on the side stream
+  constexpr size_t JB = 3 * 48;  // Jacobian P: X || Y || Z canonical
+  std::vector<uint8_t> p0(nchk * JB, 0), p1(nchk * JB, 0);
+  bool pk_inf = true;
+  for (int b = 0; b < HBH_G1_BYTES; b++) pk_inf = pk_inf && negpk[b] == 0;
   std::vector<uint32_t> i0(nchk), i1(nchk);
   for (size_t c = 0; c < ncomb; c++)
     for (size_t w = 0; w < nw; w++)
       for (int sd = 0; sd < 2; sd++) {
         const size_t k = 2 * w + sd, j = c * nw + w;
-        uint8_t* pd = (sd ? p1.data() : p0.data()) + j * HBH_G1_BYTES;
         uint32_t* qi = sd ? &i1[j] : &i0[j];
-        if (k < m) {  // (lambda_k g1, sigma_k)
-          std::memcpy(pd, lg.data() + (c * m + k) * HBH_G1_BYTES, HBH_G1_BYTES);
-          *qi = (uint32_t)(c * m + k);
-        } else {  // (-mpk, H_c), then an inactive pad (P = O)
-          if (k == m) std::memcpy(pd, negpk, HBH_G1_BYTES);
-          else std::memset(pd, 0, HBH_G1_BYTES);
-          *qi = (uint32_t)(ncomb * m + c);
+        if (k < m) {
+          *qi = (uint32_t)(c * m + k);  // (lambda_k g1, sigma_k)
+        } else {
+          if (k == m) {
+            uint8_t* d = (sd ? p1.data() : p0.data()) + j * JB;
+            std::memcpy(d, negpk, HBH_G1_BYTES);
+            d[96] = pk_inf ? 0 : 1;  // Z = 1 (Z = 0: mpk at infinity, an inactive pair)
+          }
+          *qi = (uint32_t)(ncomb * m + c);  // (-mpk, H_c), then the pad
         }
       }
+  HBH_CHECK(e->in_c.ensure(ncomb * m * 32));
+  HBH_CHECK(hipMemcpyAsync(e->in_c.p, lam.data(), ncomb * m * 32, hipMemcpyHostToDevice, s2));
   HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p0.data(), p0.size(), hipMemcpyHostToDevice, s2));
   HBH_CHECK(hipMemcpyAsync(e->in_p2.p, p1.data(), p1.size(), hipMemcpyHostToDevice, s2));
   HBH_CHECK(hipMemcpyAsync(e->in_i1.p, i0.data(), nchk * 4, hipMemcpyHostToDevice, s2));
   HBH_CHECK(hipMemcpyAsync(e->in_i2.p, i1.data(), nchk * 4, hipMemcpyHostToDevice, s2));
+  int rc = ensure_fbtab(e, s2);
+  if (rc) return rc;
+  HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, e->fbtab.p, (const uint32_t*)e->in_c.p, e->in_p1.p,
+                             e->in_p2.p));
   hbl::PairSideDesc sd0 = {e->in_p1.p, e->in_b.p, nullptr, nullptr, (const uint32_t*)e->in_i1.p, nq};
   hbl::PairSideDesc sd1 = {e->in_p2.p, e->in_b.p, nullptr, nullptr, (const uint32_t*)e->in_i2.p, nq};
   hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
-  HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1, hbl::WAVE_MILLER_ONLY, nullptr, (uint32_t*)e->fval.p));
+  HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1, hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P, nullptr,
+                             (uint32_t*)e->fval.p));
   HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, (uint8_t*)e->out_v.p));
   e->timer.end(s2, tp);
+  // the interpolation on the engine stream, concurrently with the side stream's Miller loops
+  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+  rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
+                         xs.data());
+  if (rc) return rc;
+  e->timer.end(s, tm);
   HBH_CHECK(hipEventRecord(e->join, s2));
   HBH_CHECK(hipStreamWaitEvent(s, e->join, 0));
   HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * HBH_G2_BYTES, hipMemcpyDeviceToHost, s));

@@ -544,115 +544,8 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 
 }  // extern "C"
 
-// ---------------------------------------------------------------- fixed-base g1 multiples (host)
-// The split master check of hbh_combine_verify_g2 needs lambda_k(0) * g1 for every share of a combine
-// before its Miller kernels start; on the host, with a comb table T[w][d] = d 2^(8w) g1 (32 x 255
-// affine points, 784 KiB, built once), one multiple is 32 mixed additions -- tens of microseconds for a
-// combine's 22 points, while the GPU runs the interpolation.
-namespace {
-const uint64_t G1_GEN_CANON[12] = {0xfb3af00adb22c6bbull, 0x6c55e83ff97a1aefull, 0xa14e3a3f171bac58ull,
-                                   0xc3688c4f9774b905ull, 0x2695638c4fa9ac0full, 0x17f1d3a73197d794ull,
-                                   0x0caa232946c5e7e1ull, 0xd03cc744a2888ae4ull, 0x00db18cb2c04b3edull,
-                                   0xfcf5e095d5d00af6ull, 0xa09e30ed741d8ae4ull, 0x08b3f481e3aaa0f1ull};
-struct AffG1 {
-  hh::Fq x, y;
-};
-// batch affine conversion (Montgomery's trick: one inversion); infinity -> inf[i] = true
-void batch_affine(const std::vector<hh::Jac<hh::Fq>>& p, std::vector<AffG1>& out, std::vector<bool>& inf) {
-  const size_t n = p.size();
-  out.resize(n);
-  inf.assign(n, false);
-  std::vector<hh::Fq> pre(n);
-  hh::Fq acc = hh::fq_one();
-  for (size_t i = 0; i < n; i++) {
-    inf[i] = hh::fq_is_zero(p[i].z);
-    pre[i] = acc;
-    if (!inf[i]) acc = hh::fq_mul(acc, p[i].z);
-  }
-  hh::Fq ia = hh::fq_inv(acc);
-  for (size_t i = n; i-- > 0;) {
-    if (inf[i]) continue;
-    const hh::Fq zi = hh::fq_mul(ia, pre[i]);
-    ia = hh::fq_mul(ia, p[i].z);
-    const hh::Fq zi2 = hh::fq_sqr(zi);
-    out[i].x = hh::fq_mul(p[i].x, zi2);
-    out[i].y = hh::fq_mul(p[i].y, hh::fq_mul(zi2, zi));
-  }
-}
-const std::vector<AffG1>& g1_comb() {
-  static const std::vector<AffG1> tab = [] {
-    std::vector<hh::Jac<hh::Fq>> j((size_t)32 * 255);
-    hh::Jac<hh::Fq> base = {hh::fq_from_canon(G1_GEN_CANON), hh::fq_from_canon(G1_GEN_CANON + 6), hh::fq_one()};
-    for (int w = 0; w < 32; w++) {
-      hh::Jac<hh::Fq> acc = base;
-      for (int d = 1; d <= 255; d++) {
-        j[(size_t)w * 255 + d - 1] = acc;
-        acc = hh::jac_add(acc, base);
-      }
-      for (int b = 0; b < 8; b++) base = hh::jac_dbl(base);
-    }
-    std::vector<AffG1> a;
-    std::vector<bool> inf;
-    batch_affine(j, a, inf);
-    return a;
-  }();
-  return tab;
-}
-// acc + (x, y) (madd-2007-bl, Z2 = 1)
-hh::Jac<hh::Fq> jac_add_aff(const hh::Jac<hh::Fq>& p, const AffG1& q) {
-  using namespace hh;
-  if (fq_is_zero(p.z)) return {q.x, q.y, fq_one()};
-  const Fq Z1Z1 = fq_sqr(p.z);
-  const Fq U2 = fq_mul(q.x, Z1Z1);
-  const Fq S2 = fq_mul(fq_mul(q.y, p.z), Z1Z1);
-  const Fq H = fq_sub(U2, p.x);
-  Fq r = fq_sub(S2, p.y);
-  if (fq_is_zero(H)) {
-    if (fq_is_zero(r)) return jac_dbl(Jac<Fq>{q.x, q.y, fq_one()});
-    return jac_inf<Fq>();
-  }
-  const Fq HH = fq_sqr(H);
-  const Fq I = fq_add(fq_add(HH, HH), fq_add(HH, HH));
-  const Fq J = fq_mul(H, I);
-  r = fq_add(r, r);
-  const Fq V = fq_mul(p.x, I);
-  Jac<Fq> o;
-  o.x = fq_sub(fq_sub(fq_sqr(r), J), fq_add(V, V));
-  const Fq YJ = fq_mul(p.y, J);
-  o.y = fq_sub(fq_mul(r, fq_sub(V, o.x)), fq_add(YJ, YJ));
-  o.z = fq_sub(fq_sub(fq_sqr(fq_add(p.z, H)), Z1Z1), HH);
-  return o;
-}
-}  // namespace
-
-// Not part of the public ABI (engine.hip's split master check): out[i] = k_i * g1 (ABI affine, 96 B;
-// k_i 32-byte LE, any 256-bit integer), and neg_out = -pk for the ABI point pk (infinity stays).
-extern "C" int hbh__host_g1_gen_mul(size_t n, const uint8_t* scalars, uint8_t* out) {
-  if (n == 0) return HBH_OK;
-  const std::vector<AffG1>& tab = g1_comb();
-  std::vector<hh::Jac<hh::Fq>> acc(n);
-  const int threads = (int)std::min<size_t>(hh::usable_cpus(), (n + 7) / 8);
-  hh::parallel_for(n, threads, [&](size_t i) {
-    hh::Jac<hh::Fq> a = hh::jac_inf<hh::Fq>();
-    const uint8_t* k = scalars + i * 32;
-    for (int w = 0; w < 32; w++)
-      if (k[w]) a = jac_add_aff(a, tab[(size_t)w * 255 + k[w] - 1]);
-    acc[i] = a;
-  });
-  std::vector<AffG1> aff;
-  std::vector<bool> inf;
-  batch_affine(acc, aff, inf);
-  for (size_t i = 0; i < n; i++) {
-    uint8_t* o = out + i * HBH_G1_BYTES;
-    if (inf[i]) {
-      memset(o, 0, HBH_G1_BYTES);
-      continue;
-    }
-    hh::fq_to_le(aff[i].x, o);
-    hh::fq_to_le(aff[i].y, o + 48);
-  }
-  return HBH_OK;
-}
+// Not part of the public ABI (engine.hip's split master check of hbh_combine_verify_g2): neg_out = -pk
+// for the ABI point pk (infinity stays all-zero).
 extern "C" int hbh__host_g1_neg(const uint8_t* pk, uint8_t* neg_out) {
   hh::Jac<hh::Fq> p;
   if (!hh::g1_from_abi(pk, p)) return host_fail(HBH_ERR_ARG, "coordinate >= p");

@@ -376,9 +376,63 @@ __global__ void __launch_bounds__(64) k_interp_g1_join(int ncomb, const int32_t*
   }
 }
 
+// lambda_k g1 for the split master check of hbh_combine_verify_g2 (latency, not throughput): one
+// 64-lane workgroup per scalar; quad g adds the comb-table points of scalar bytes 2g and 2g + 1 (a
+// mixed addition), then four levels of general additions through LDS sum the 16 quads (depth 5 group
+// operations of 5 product rounds each instead of 32 sequential additions); quad 0 writes the Jacobian
+// sum (no inversion) as point p = (c, k) of combine c to side k & 1 of wave c * nw + k / 2 -- the P
+// arrays the Miller-only k_wave launch reads (WAVE_JAC_P).
+__global__ void __launch_bounds__(64) k_g1_gen_quad(int n, int m, int nw, const uint32_t* __restrict__ tab,
+                                                    const uint32_t* __restrict__ scalars, uint32_t* __restrict__ out0,
+                                                    uint32_t* __restrict__ out1) {
+  __shared__ int32_t sm[16 * Q_JROW_WORDS];
+  const int p = blockIdx.x;
+  if (p >= n) return;  // uniform per workgroup
+  const int g = threadIdx.x >> 2;
+  QJ acc = qj_inf();
+#pragma unroll 1
+  for (int h = 0; h < 2; h++) {
+    const int w = 2 * g + h;
+    const uint32_t d = (scalars[(size_t)p * 8 + (w >> 2)] >> (8 * (w & 3))) & 0xffu;
+    if (d) {
+      Fp x, y;
+      load_aff(tab + ((size_t)w * Q_FB_ROW + d) * Q_G1_WORDS, x, y);
+      acc = g1q_add_affine(acc, x, y);
+    }
+  }
+  if (q_lane() == 0) qj_store(sm + g * Q_JROW_WORDS, acc);
+  __syncthreads();
+  for (int s = 8; s > 0; s >>= 1) {
+    if (g < s) acc = g1q_add(qj_load(sm + g * Q_JROW_WORDS), qj_load(sm + (g + s) * Q_JROW_WORDS));
+    __syncthreads();
+    if (g < s && q_lane() == 0) qj_store(sm + g * Q_JROW_WORDS, acc);
+    __syncthreads();
+  }
+  if (g != 0) return;
+  const int c = p / m, k = p % m;
+  uint32_t* o = ((k & 1) ? out1 : out0) + ((size_t)c * nw + k / 2) * 36;
+  if (qj_zero(acc)) {
+    if (q_lane() == 0)
+      for (int i = 0; i < 36; i++) o[i] = 0u;
+    return;
+  }
+  // Jacobian out (the Miller kernel scales its lines by Z^3 instead of inverting Z); the quad's
+  // lanes 0-2 convert one coordinate each
+  const int q = q_lane();
+  if (q < 3) fp_to_words(q == 0 ? acc.x : (q == 1 ? acc.y : acc.z), o + 12 * q);
+}
+
 }  // namespace hbs
 
 namespace hbl {
+
+hipError_t g1_gen_tree(hipStream_t s, int n, int m, int nw, const void* tab, const uint32_t* scalars, void* out0,
+                       void* out1) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hbs::k_g1_gen_quad, dim3((unsigned)n), dim3(64), 0, s, n, m, nw, (const uint32_t*)tab, scalars,
+                     (uint32_t*)out0, (uint32_t*)out1);
+  return hipGetLastError();
+}
 
 size_t interp_g1_quad_part_bytes(int ncomb) { return (size_t)ncomb * hbs::G1Q_NCHUNK * hbs::Q_JROW_WORDS * 4; }
 

@@ -38,7 +38,8 @@ struct WaveSide {
 struct WaveArgs {
   int n;
   WaveSide s[2];
-  int flags;            // bit 0: negate P2; bit 1: conjugated value (single pairing); bit 2: Miller only
+  int flags;            // bit 0: negate P2; bit 1: conjugated value (single pairing); bit 2: Miller only;
+                        // bit 3: Jacobian P (36 words, both sides WALK)
   uint8_t* verdict;
   uint32_t* value_out;  // 144 canonical words per check (may be null)
   const uint32_t* fin;  // product mode: nf Miller values (144 words, w-basis) per check; null otherwise
@@ -391,7 +392,7 @@ HP_D void put_const(uint32_t* sm, int h, int slot, const uint32_t (&c0)[NL], con
   st_own(sm, slot, h, v);
 }
 
-// side K of check i: writes its slots (pair K: XP, YP; pair 2 + K: QX, QY, T), returns the line
+// side K of check i: writes its slots (pair K: XP, YP (ZP); pair 2 + K: QX, QY, T), returns the line
 // table of a TABLE side; bad = Q index out of range
 template <int K>
 HP_D const int4* wave_side(const WaveArgs& a, uint32_t* sm, int i, int h, int pair, bool& act, bool& bad) {
@@ -402,8 +403,16 @@ HP_D const int4* wave_side(const WaveArgs& a, uint32_t* sm, int i, int h, int pa
   if (bad) return nullptr;
   const bool neg = K == 1 && (a.flags & 1);
   bool pinf = false;
-  Fp xp, yp;
-  if (s.p) {
+  Fp xp, yp, zp3;
+  if (s.p && (a.flags & 8)) {  // Jacobian P (X, Y, Z; Z = 0 at infinity): XP = X Z, YP = Y, ZP = Z^3
+    const uint32_t* w = s.p + (size_t)i * 36;
+    pinf = words_zero(w + 24, 12);
+    const Fp z = fp_from_words(w + 24);
+    xp = fp_mul(fp_from_words(w), z);
+    yp = fp_from_words(w + 12);
+    zp3 = fp_mul(fp_sqr(z), z);
+    if (neg) yp = fp_neg(yp);
+  } else if (s.p) {
     const uint32_t* w = s.p + (size_t)i * 24;
     pinf = words_zero(w, 24);
     xp = fp_from_words(w);
@@ -439,6 +448,7 @@ HP_D const int4* wave_side(const WaveArgs& a, uint32_t* sm, int i, int h, int pa
   if (pair == K) {
     st_own(sm, base + 0, h, h ? fp_zero() : xp);
     st_own(sm, base + 1, h, h ? fp_zero() : yp);
+    if (s.p && (a.flags & 8)) st_own(sm, base + 7, h, h ? fp_zero() : zp3);
   }
   act = !pinf && !qinf;
   return tl;
@@ -506,7 +516,7 @@ __global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
       return;
     }
     __syncthreads();
-    const int mv = (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
+    const int mv = (a.flags & 8) ? 4 : (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
     run_stages(sm, hbw::WP_MILLER_OFF[mv], hbw::WP_MILLER_N[mv], h, pair, act0, act1, tl0, tl1);
     if (a.flags & 4) {  // Miller only: f (w-basis) out, no final exponentiation
       if (pair < 6 && a.value_out)

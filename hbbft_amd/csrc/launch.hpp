@@ -42,6 +42,9 @@ hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairS
 // w-basis) to value_out and stops there; wave_prod_fe then verifies prod_k fin[i][k] (nf values per
 // check) with one final exponentiation: verdict[i] = (FE(prod) == 1).
 constexpr int WAVE_MILLER_ONLY = 4;
+// flags bit 3 (WAVE_JAC_P): every P is Jacobian, X || Y || Z canonical (36 words, Z = 0 at infinity);
+// both sides must WALK.  The lines are scaled by Z^3, so no inversion of Z is needed.
+constexpr int WAVE_JAC_P = 8;
 hipError_t wave_prod_fe(hipStream_t s, int n, int nf, const uint32_t* fin, uint8_t* verdict);
 
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
@@ -77,6 +80,11 @@ hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const u
 size_t fb_table_bytes();
 hipError_t fb_table(hipStream_t s, void* tab);
 hipError_t g1_mul_gen(hipStream_t s, int n, const void* tab, const uint32_t* scalars, void* out);
+// lambda_k g1 (scalars 8 LE words each, n = ncomb * m) by a 5-level tree over the comb table, in
+// Jacobian form (36 words: X || Y || Z canonical, all zero at infinity) to out0 / out1 (even / odd k) at
+// wave c * nw + k / 2: the P sides of the split master check (k_wave with WAVE_JAC_P)
+hipError_t g1_gen_tree(hipStream_t s, int n, int m, int nw, const void* tab, const uint32_t* scalars, void* out0,
+                       void* out1);
 // xs[k] = idx[k] + 1 for n = ncomb * m device-resident indices; status[k / m] = HBL_BAD_INDEX for
 // an index of 0xffffffff (status zeroed by the caller beforehand).
 hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint32_t* xs, int* status);

@@ -111,3 +111,30 @@ def test_split_master_check(progs):
     f = W.emulate_miller(v, [(P[0], Q[0], False), (None, Q[1], False)])
     g = W.emulate_miller(v, [(mpk, C.G2_GEN, True), (None, Q[2], False)])
     assert W.emulate_prod_fe(v, [f, g]) == ONE_W
+
+
+def test_split_master_check_jacobian_p(progs):
+    """Mode WWJ (the split master check's lambda_k g1 straight from the device tree, no inversion):
+    P = (X, Y, Z) Jacobian; the Miller value differs from the affine one by an Fp factor, the final
+    exponentiation's output does not."""
+    rnd = random.Random(9)
+    a = [rnd.randrange(1, C.R) for _ in range(3)]
+    b = [rnd.randrange(1, C.R) for _ in range(3)]
+    c = sum(x * y for x, y in zip(a, b)) % C.R
+    vj, v = progs["variants"]["WWJ"], progs["variants"]["WW"]
+
+    def jac(pt):
+        z = rnd.randrange(1, C.P)
+        return ("JAC", (pt[0] * z * z % C.P, pt[1] * z * z * z % C.P, z))
+
+    P = [C.g1_mul(C.G1_GEN, x) for x in a]
+    Q = [C.g2_mul(C.G2_GEN, y) for y in b]
+    mpk = C.g1_mul(C.G1_GEN, c)
+    negmpk = (mpk[0], (-mpk[1]) % C.P)
+    fs = [W.emulate_miller(vj, [(jac(P[0]), Q[0], False), (jac(P[1]), Q[1], False)]),
+          W.emulate_miller(vj, [(jac(P[2]), Q[2], False), (("JAC", (negmpk[0], negmpk[1], 1)), C.G2_GEN, False)])]
+    assert W.emulate_prod_fe(v, fs) == ONE_W
+    # a Jacobian P at infinity (Z = 0) is an inactive pair; the same value as the affine program
+    f = W.emulate_miller(vj, [(jac(P[0]), Q[0], False), (("JAC", (1, 1, 0)), Q[1], False)])
+    g = W.emulate_miller(v, [(P[0], Q[0], False), (None, Q[1], False)])
+    assert W.emulate_prod_fe(v, [f]) == W.emulate_prod_fe(v, [g])

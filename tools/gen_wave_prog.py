@@ -37,7 +37,7 @@ SPECIAL_CYC = 2  # a run of cyclotomic squarings kept in registers (k_wave.hip c
 
 # fixed slot map shared with the kernel prologue
 CONSTS = ["ZERO", "ONE"] + ["F1_%d" % k for k in range(6)] + ["F2_%d" % k for k in range(6)] + ["G1X", "G1Y", "G1NY"]
-SIDE_FIELDS = ["XP", "YP", "QX", "QY", "TX", "TY", "TZ"]
+SIDE_FIELDS = ["XP", "YP", "QX", "QY", "TX", "TY", "TZ", "ZP"]  # ZP: Z^3 of a Jacobian P (mode WWJ)
 MULF_G = ["S0_" + f for f in SIDE_FIELDS[:6]]
 
 
@@ -267,6 +267,11 @@ class Builder:
 
     # ---- Miller loop (k_pair.hip k_pair_verify): sides = ('W' | 'T', 'W' | 'T')
     def miller(self, modes):
+        """modes[side] = 'W' (walk Q in the program) or 'T' (table lines); modes of length 3 ending in
+        'J' (WWJ): both P given in Jacobian form (X, Y, Z): the kernel stores XP = X Z, YP = Y and
+        ZP = Z^3, and every line's c0 is multiplied by ZP -- the line scaled by Z^3 (an Fp factor the
+        final exponentiation removes), so P needs no inversion (the split master check's lambda_k g1)."""
+        jac = len(modes) == 3 and modes[2] == "J"
         steps = []
         for b in range(62, -1, -1):
             steps.append("D")
@@ -299,16 +304,20 @@ class Builder:
                             [Out(T("E"), [(P_(0), 3, 0)]), Out(T("B"), [(P_(1), 1, 0)]),
                              Out(T("ZZ"), [(P_(2), 1, 0)]),
                              Out(TZ, [(P_(3), 1, 0), (P_(1), -1, 0), (P_(2), -1, 0)])], name="dbl1"))
+                l0 = T("L0R") if jac else l[0]
                 self.add(Op("M1", [[Prod(T("B"), T("B"))], [Prod(TX, T("B"))], [Prod(T("E"), T("E"))],
                                    [Prod(T("E"), TX)], [Prod(T("E"), T("ZZ"))], [Prod(TZ, T("ZZ"))]],
                             [Out(T("C"), [(P_(0), 1, 0)]), Out(T("D"), [(P_(1), 4, 0)]),
                              Out(TX, [(P_(2), 1, 0), (P_(1), -8, 0)]),
-                             Out(l[0], [(P_(3), 1, 0), (T("B"), -2, 0)], gate=side, default="ONE"),
+                             Out(l0, [(P_(3), 1, 0), (T("B"), -2, 0)], **({} if jac else dict(gate=side, default="ONE"))),
                              Out(T("LC1"), [(P_(4), -1, 0)]), Out(T("LC4"), [(P_(5), 1, 0)])], name="dbl2"))
-                self.add(Op("M1", [[Prod(T("E"), T("D"), d=TX, sd=-1)], [Prod(T("LC1"), XP)], [Prod(T("LC4"), YP)]],
-                            [Out(TY, [(P_(0), 1, 0), (T("C"), -8, 0)]),
-                             Out(l[1], [(P_(1), 1, 0)], gate=side), Out(l[2], [(P_(2), 1, 0)], gate=side)],
-                            name="dbl3"))
+                prods = [[Prod(T("E"), T("D"), d=TX, sd=-1)], [Prod(T("LC1"), XP)], [Prod(T("LC4"), YP)]]
+                outs = [Out(TY, [(P_(0), 1, 0), (T("C"), -8, 0)]),
+                        Out(l[1], [(P_(1), 1, 0)], gate=side), Out(l[2], [(P_(2), 1, 0)], gate=side)]
+                if jac:
+                    prods.append([Prod(l0, S(side, "ZP"))])
+                    outs.append(Out(l[0], [(P_(3), 1, 0)], gate=side, default="ONE"))
+                self.add(Op("M1", prods, outs, name="dbl3"))
             else:
                 # h_add_step (mixed addition with the affine Q)
                 self.add(Op("M1", [[Prod(TZ, TZ)], [Prod(QY, TZ)]],
@@ -320,15 +329,20 @@ class Builder:
                                    [Prod(T("R"), QX)]],
                             [Out(T("HH"), [(P_(0), 1, 0)]), Out(T("RR"), [(P_(1), 1, 0)]), Out(TZ, [(P_(2), 1, 0)]),
                              Out(T("RXQ"), [(P_(3), 1, 0)])], name="add3"))
+                l0 = T("L0R") if jac else l[0]
                 self.add(Op("M1", [[Prod(T("H"), T("HH"))], [Prod(TX, T("HH"))], [Prod(QY, TZ)],
                                    [Prod(T("R"), XP)], [Prod(TZ, YP)]],
                             [Out(T("HHH"), [(P_(0), 1, 0)]), Out(T("V"), [(P_(1), 1, 0)]),
                              Out(TX, [(T("RR"), 1, 0), (P_(0), -1, 0), (P_(1), -2, 0)]),
-                             Out(l[0], [(T("RXQ"), 1, 0), (P_(2), -1, 0)], gate=side, default="ONE"),
+                             Out(l0, [(T("RXQ"), 1, 0), (P_(2), -1, 0)], **({} if jac else dict(gate=side, default="ONE"))),
                              Out(l[1], [(P_(3), -1, 0)], gate=side), Out(l[2], [(P_(4), 1, 0)], gate=side)],
                             name="add4"))
-                self.add(Op("M1", [[Prod(T("R"), T("V"), d=TX, sd=-1)], [Prod(TY, T("HHH"))]],
-                            [Out(TY, [(P_(0), 1, 0), (P_(1), -1, 0)])], name="add5"))
+                prods = [[Prod(T("R"), T("V"), d=TX, sd=-1)], [Prod(TY, T("HHH"))]]
+                outs = [Out(TY, [(P_(0), 1, 0), (P_(1), -1, 0)])]
+                if jac:
+                    prods.append([Prod(l0, S(side, "ZP"))])
+                    outs.append(Out(l[0], [(P_(2), 1, 0)], gate=side, default="ONE"))
+                self.add(Op("M1", prods, outs, name="add5"))
 
         for side in (0, 1):
             walk(side, 0)
@@ -720,7 +734,11 @@ def _setup(prog, sides):
     act = []
     tables = []
     for k, (Pk, Qk, neg) in enumerate(sides):
-        if Pk == "GEN":
+        zp = 1
+        if isinstance(Pk, tuple) and Pk and Pk[0] == "JAC":  # Jacobian (X, Y, Z): XP = X Z, YP = Y, ZP = Z^3
+            X, Y, Z = Pk[1]
+            xp, yp, zp, pinf = X * Z % P, Y, pow(Z, 3, P), Z % P == 0
+        elif Pk == "GEN":
             xp, yp = const_values()["G1X"][0], const_values()["G1Y"][0]
             pinf = False
         elif Pk is None:
@@ -731,6 +749,7 @@ def _setup(prog, sides):
             yp = (-yp) % P
         mem[S["S%d_XP" % k]] = (xp, 0)
         mem[S["S%d_YP" % k]] = (yp, 0)
+        mem[S["S%d_ZP" % k]] = (zp, 0)
         xq, yq = Qk if Qk is not None else ((1, 0), (1, 0))
         mem[S["S%d_QX" % k]] = xq
         mem[S["S%d_QY" % k]] = yq
@@ -853,7 +872,7 @@ def emulate_prod_fe(prog, fs):
 
 
 # ------------------------------------------------------------------------------- build / emit
-MODES = ["WW", "WT", "TW", "TT"]
+MODES = ["WW", "WT", "TW", "TT", "WWJ"]
 
 
 def allocate(b, stages):
@@ -911,7 +930,7 @@ def build():
     nslots = max(fe.slots.values()) + 1
     for m in MODES:
         b = Builder(m)
-        b.miller((m[0], m[1]))
+        b.miller(tuple(m))
         st = schedule(b.ops)
         b.slots = allocate(b, st)
         nslots = max(nslots, max(b.slots.values()) + 1)
@@ -968,9 +987,10 @@ def emit(out, path):
     lines.append("constexpr int WP_FE_OFF = %d, WP_FE_N = %d;" % (fe_off, fe_n))
     lines.append("// F <- F * G with G in side 0's slots XP YP QX QY TX TY (product of partial Miller values)")
     lines.append("constexpr int WP_MULF_OFF = %d, WP_MULF_N = %d;" % (mf_off, mf_n))
-    lines.append("// Miller programs: WALK/TABLE for side 0 and side 1 -> index (side0 is TABLE) * 2 + (side1 is TABLE)")
-    lines.append("constexpr int WP_MILLER_OFF[4] = {%s};" % ", ".join(str(i[0]) for i in info))
-    lines.append("constexpr int WP_MILLER_N[4] = {%s};" % ", ".join(str(i[1]) for i in info))
+    lines.append("// Miller programs: WALK/TABLE for side 0 and side 1 -> index (side0 is TABLE) * 2 + (side1 is TABLE);")
+    lines.append("// index 4: both sides WALK with Jacobian P (XP = X Z, YP = Y, ZP = Z^3)")
+    lines.append("constexpr int WP_MILLER_OFF[5] = {%s};" % ", ".join(str(i[0]) for i in info))
+    lines.append("constexpr int WP_MILLER_N[5] = {%s};" % ", ".join(str(i[1]) for i in info))
 
     def arr(name, typ, vals, per):
         lines.append("__device__ __attribute__((aligned(16))) const %s %s[%d] = {" % (typ, name, len(vals)))
