@@ -114,7 +114,9 @@ struct hbh_engine {
   // the engine stream interpolates; partial Miller values in fval
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
-  DevBuf fval;
+  DevBuf fval, split_in, split_out;
+  uint8_t* h_stage = nullptr;  // pinned host staging of the split check (one upload, one download)
+  size_t h_stage_cap = 0;
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
 };
 
@@ -291,8 +293,10 @@ int hbh_engine_destroy(hbh_engine* e) {
   e->timer.clear();
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
-                    &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval})
+                    &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval, &e->split_in,
+                    &e->split_out})
     b->release();
+  if (e->h_stage) (void)hipHostFree(e->h_stage);
   (void)hipEventDestroy(e->done);
   (void)hipEventDestroy(e->fork);
   (void)hipEventDestroy(e->join);
@@ -629,6 +633,25 @@ void host_lagrange(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* lam, in
   }
 }
 
+// the four GLS digits (base |x|) of n canonical scalars (4 x u64 each): q <- q / |x| three times, digit j
+// = remainder, digit 3 = the last quotient
+void host_gls_digits(const uint64_t* lam, size_t n, uint64_t* dg) {
+  constexpr uint64_t XA = 0xd201000000010000ull;
+  for (size_t k = 0; k < n; k++) {
+    uint64_t q[4] = {lam[k * 4], lam[k * 4 + 1], lam[k * 4 + 2], lam[k * 4 + 3]};
+    for (int j = 0; j < 3; j++) {
+      u128 rem = 0;
+      for (int w = 3; w >= 0; w--) {
+        const u128 cur = (rem << 64) | q[w];
+        q[w] = (uint64_t)(cur / XA);
+        rem = cur % XA;
+      }
+      dg[k * 4 + j] = (uint64_t)rem;
+    }
+    dg[k * 4 + 3] = q[0];
+  }
+}
+
 void host_interp_digits(const uint32_t* xs, size_t ncomb, size_t m, uint64_t* digits, int* status, bool g1 = false) {
   constexpr uint64_t XA = 0xd201000000010000ull;
   host_lagrange(xs, ncomb, m, digits, status);  // in place: lambda_k's 4 words become its 4 digits
@@ -787,92 +810,93 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
                          const uint8_t* shares, const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out,
                          int* status, uint8_t* verdicts) {
   const size_t np = m + 1, nw = (np + 1) / 2, nchk = ncomb * nw, nq = ncomb * np;
-  std::vector<uint64_t> lam(ncomb * m * 4);
-  std::vector<int> lst(ncomb);
-  host_lagrange(xs.data(), ncomb, m, lam.data(), lst.data());
+  constexpr size_t JB = 3 * 48;  // Jacobian P: X || Y || Z canonical
   uint8_t negpk[HBH_G1_BYTES];
   if (hbh__host_g1_neg(master_pk, negpk)) return fail(HBH_ERR_ARG, "master key coordinate >= p");
-  std::lock_guard<std::mutex> lk(e->mu);
-  HBH_CHECK(hipSetDevice(e->device));
-  hipStream_t s = e->stream, s2 = e->side;
-  {
-    const int rc_ = begin_call(e, s);
-    if (rc_) return rc_;
-  }
-  // Q table: the shares, then one H per combine (the interpolation reads the shares' prefix)
-  HBH_CHECK(e->in_a.ensure(ncomb * m * 4));
-  HBH_CHECK(e->in_b.ensure(nq * HBH_G2_BYTES));
-  HBH_CHECK(e->out_x.ensure(ncomb * HBH_G2_BYTES));
-  HBH_CHECK(e->status.ensure(ncomb * sizeof(int)));
-  HBH_CHECK(e->out_v.ensure(ncomb));
-  HBH_CHECK(e->in_p1.ensure(nchk * 3 * 48));
-  HBH_CHECK(e->in_p2.ensure(nchk * 3 * 48));
-  HBH_CHECK(e->in_i1.ensure(nchk * 4));
-  HBH_CHECK(e->in_i2.ensure(nchk * 4));
-  HBH_CHECK(e->fval.ensure(nchk * 144 * 4));
-  HBH_CHECK(hipMemcpyAsync(e->in_a.p, xs.data(), ncomb * m * 4, hipMemcpyHostToDevice, s));
-  HBH_CHECK(hipMemcpyAsync(e->in_b.p, shares, ncomb * m * HBH_G2_BYTES, hipMemcpyHostToDevice, s));
-  HBH_CHECK(hipMemcpyAsync((uint8_t*)e->in_b.p + ncomb * m * HBH_G2_BYTES, hashes, ncomb * HBH_G2_BYTES,
-                           hipMemcpyHostToDevice, s));
-  HBH_CHECK(hipMemsetAsync(e->status.p, 0, ncomb * sizeof(int), s));
-  HBH_CHECK(hipEventRecord(e->fork, s));
-  HBH_CHECK(hipStreamWaitEvent(s2, e->fork, 0));
-  // the two sides of every wave: (-mpk, H_c) and the inactive pad (P = O) from the host, lambda_k g1
-  // written over the zero entries by k_g1_gen_tree on the side stream
-  constexpr size_t JB = 3 * 48;  // Jacobian P: X || Y || Z canonical
-  std::vector<uint8_t> p0(nchk * JB, 0), p1(nchk * JB, 0);
   bool pk_inf = true;
   for (int b = 0; b < HBH_G1_BYTES; b++) pk_inf = pk_inf && negpk[b] == 0;
-  std::vector<uint32_t> i0(nchk), i1(nchk);
+  // one upload: Q table (shares, then one H per combine) | GLS digits | lambdas | P sides | Q indices
+  const size_t o_q = 0, o_dg = o_q + nq * HBH_G2_BYTES, o_lam = o_dg + ncomb * m * 32, o_p0 = o_lam + ncomb * m * 32,
+               o_p1 = o_p0 + nchk * JB, o_i0 = o_p1 + nchk * JB, o_i1 = o_i0 + nchk * 4, in_bytes = o_i1 + nchk * 4;
+  // one download: signatures | verdicts
+  const size_t o_v = ncomb * HBH_G2_BYTES, out_bytes = o_v + ncomb;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HBH_CHECK(hipSetDevice(e->device));
+  const size_t stage_bytes = std::max(in_bytes, out_bytes);
+  if (stage_bytes > e->h_stage_cap) {
+    if (e->h_stage) HBH_CHECK(hipHostFree(e->h_stage));
+    e->h_stage = nullptr;
+    e->h_stage_cap = 0;
+    HBH_CHECK(hipHostMalloc((void**)&e->h_stage, stage_bytes + stage_bytes / 4 + 4096, hipHostMallocDefault));
+    e->h_stage_cap = stage_bytes + stage_bytes / 4 + 4096;
+  }
+  uint8_t* hs = e->h_stage;
+  std::memcpy(hs + o_q, shares, ncomb * m * HBH_G2_BYTES);
+  std::memcpy(hs + o_q + ncomb * m * HBH_G2_BYTES, hashes, ncomb * HBH_G2_BYTES);
+  std::vector<int> lst(ncomb);
+  host_lagrange(xs.data(), ncomb, m, (uint64_t*)(hs + o_lam), lst.data());
+  host_gls_digits((const uint64_t*)(hs + o_lam), ncomb * m, (uint64_t*)(hs + o_dg));
+  std::memset(hs + o_p0, 0, 2 * nchk * JB);
+  uint32_t* i0 = (uint32_t*)(hs + o_i0);
+  uint32_t* i1 = (uint32_t*)(hs + o_i1);
   for (size_t c = 0; c < ncomb; c++)
     for (size_t w = 0; w < nw; w++)
       for (int sd = 0; sd < 2; sd++) {
         const size_t k = 2 * w + sd, j = c * nw + w;
         uint32_t* qi = sd ? &i1[j] : &i0[j];
         if (k < m) {
-          *qi = (uint32_t)(c * m + k);  // (lambda_k g1, sigma_k)
+          *qi = (uint32_t)(c * m + k);  // (lambda_k g1, sigma_k): P written by k_g1_gen_quad
         } else {
-          if (k == m) {
-            uint8_t* d = (sd ? p1.data() : p0.data()) + j * JB;
+          if (k == m) {  // (-mpk, H_c) with Z = 1 (Z = 0: mpk at infinity, an inactive pair)
+            uint8_t* d = hs + (sd ? o_p1 : o_p0) + j * JB;
             std::memcpy(d, negpk, HBH_G1_BYTES);
-            d[96] = pk_inf ? 0 : 1;  // Z = 1 (Z = 0: mpk at infinity, an inactive pair)
+            d[96] = pk_inf ? 0 : 1;
           }
-          *qi = (uint32_t)(ncomb * m + c);  // (-mpk, H_c), then the pad
+          *qi = (uint32_t)(ncomb * m + c);  // then an inactive pad (P = O)
         }
       }
-  HBH_CHECK(e->in_c.ensure(ncomb * m * 32));
-  HBH_CHECK(hipMemcpyAsync(e->in_c.p, lam.data(), ncomb * m * 32, hipMemcpyHostToDevice, s2));
-  HBH_CHECK(hipMemcpyAsync(e->in_p1.p, p0.data(), p0.size(), hipMemcpyHostToDevice, s2));
-  HBH_CHECK(hipMemcpyAsync(e->in_p2.p, p1.data(), p1.size(), hipMemcpyHostToDevice, s2));
-  HBH_CHECK(hipMemcpyAsync(e->in_i1.p, i0.data(), nchk * 4, hipMemcpyHostToDevice, s2));
-  HBH_CHECK(hipMemcpyAsync(e->in_i2.p, i1.data(), nchk * 4, hipMemcpyHostToDevice, s2));
+  hipStream_t s = e->stream, s2 = e->side;
+  {
+    const int rc_ = begin_call(e, s);
+    if (rc_) return rc_;
+  }
+  HBH_CHECK(e->split_in.ensure(in_bytes));
+  HBH_CHECK(e->split_out.ensure(out_bytes));
+  HBH_CHECK(e->fval.ensure(nchk * 144 * 4));
+  HBH_CHECK(e->ipart.ensure(hbl::interp_g2_pair_part_bytes((int)ncomb)));
+  uint8_t* din = (uint8_t*)e->split_in.p;
+  uint8_t* dout = (uint8_t*)e->split_out.p;
+  HBH_CHECK(hipMemcpyAsync(din, hs, in_bytes, hipMemcpyHostToDevice, s));
+  HBH_CHECK(hipEventRecord(e->fork, s));
+  HBH_CHECK(hipStreamWaitEvent(s2, e->fork, 0));
+  // side stream: lambda_k g1 (Jacobian, over the zero P entries), the m + 1 Miller loops, the product
+  // and the final exponentiation
   int rc = ensure_fbtab(e, s2);
   if (rc) return rc;
-  HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, e->fbtab.p, (const uint32_t*)e->in_c.p, e->in_p1.p,
-                             e->in_p2.p));
-  hbl::PairSideDesc sd0 = {e->in_p1.p, e->in_b.p, nullptr, nullptr, (const uint32_t*)e->in_i1.p, nq};
-  hbl::PairSideDesc sd1 = {e->in_p2.p, e->in_b.p, nullptr, nullptr, (const uint32_t*)e->in_i2.p, nq};
+  HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, e->fbtab.p, (const uint32_t*)(din + o_lam),
+                             din + o_p0, din + o_p1));
+  hbl::PairSideDesc sd0 = {din + o_p0, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i0), nq};
+  hbl::PairSideDesc sd1 = {din + o_p1, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i1), nq};
   hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
   HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1, hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P, nullptr,
                              (uint32_t*)e->fval.p));
-  HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, (uint8_t*)e->out_v.p));
+  HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, dout + o_v));
   e->timer.end(s2, tp);
-  // the interpolation on the engine stream, concurrently with the side stream's Miller loops
+  // engine stream, concurrently: the interpolation (lane-quad latency form, host digits)
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  rc = launch_combine_g2(e, s, ncomb, m, (const uint32_t*)e->in_a.p, e->in_b.p, e->out_x.p, (int*)e->status.p,
-                         xs.data());
-  if (rc) return rc;
+  HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)(din + o_dg), din + o_q, e->ipart.p, dout));
   e->timer.end(s, tm);
   HBH_CHECK(hipEventRecord(e->join, s2));
   HBH_CHECK(hipStreamWaitEvent(s, e->join, 0));
-  HBH_CHECK(hipMemcpyAsync(out, e->out_x.p, ncomb * HBH_G2_BYTES, hipMemcpyDeviceToHost, s));
-  HBH_CHECK(hipMemcpyAsync(status, e->status.p, ncomb * sizeof(int), hipMemcpyDeviceToHost, s));
-  HBH_CHECK(hipMemcpyAsync(verdicts, e->out_v.p, ncomb, hipMemcpyDeviceToHost, s));
+  HBH_CHECK(hipMemcpyAsync(hs, dout, out_bytes, hipMemcpyDeviceToHost, s));
   {
     const int rc_ = end_call(e, s);
     if (rc_) return rc_;
   }
   HBH_CHECK(hipStreamSynchronize(s));
+  std::memcpy(out, hs, ncomb * HBH_G2_BYTES);
+  std::memcpy(verdicts, hs + o_v, ncomb);
+  for (size_t c = 0; c < ncomb; c++) status[c] = lst[c];
   return HBH_OK;
 }
 }  // namespace
@@ -912,7 +936,7 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
     if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
     xs[k] = idx[k] + 1;
   }
-  if (ncomb <= HBH_SPLIT_CHECK_MAX && e->split_check)
+  if (ncomb <= HBH_SPLIT_CHECK_MAX && e->split_check && hbl::interp_g2_pair_fits((int)m))
     return combine_verify_split(e, ncomb, m, xs, shares, master_pk, hashes, out, status, verdicts);
   // P1 = master pk (one record per combine), P2 = the G1 generator (a flag, nothing uploaded)
   std::vector<uint8_t> p12(ncomb * HBH_G1_BYTES);
