@@ -111,7 +111,10 @@ struct hbh_engine {
   // staging for host-pointer entry points
   DevBuf in_p1, in_q1, in_i1, in_p2, in_q2, in_i2, out_v, in_a, in_b, in_c, in_d, out_x;
   // split master check (hbh_combine_verify_g2): a second stream runs the partial Miller loops while
-  // the engine stream interpolates; partial Miller values in fval
+  // the engine stream interpolates; partial Miller values in fval.  Created on the first split call:
+  // HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues round-robin, and an idle extra stream
+  // made at engine creation put the caller's two alternating verify streams on one queue
+  // (sign bench: 23.3 instead of 21.1 ms per 65,536-check step)
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   DevBuf fval, split_in, split_out;
@@ -269,11 +272,7 @@ int hbh_engine_create(int device, hbh_engine** out) {
     err = hipEventCreateWithFlags(&e->slot_done[k], hipEventDisableTiming);
     if (err == hipSuccess) err = hipEventRecord(e->slot_done[k], e->stream);
   }
-  if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
-  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->fork, hipEventDisableTiming);
-  if (err == hipSuccess) err = hipEventCreateWithFlags(&e->join, hipEventDisableTiming);
   if (err != hipSuccess) {
-    if (e->side) (void)hipStreamDestroy(e->side);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return fail(HBH_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(err));
@@ -289,7 +288,7 @@ int hbh_engine_destroy(hbh_engine* e) {
   for (hipEvent_t ev : e->slot_done)
     if (ev) (void)hipEventSynchronize(ev);
   (void)hipStreamSynchronize(e->stream);
-  (void)hipStreamSynchronize(e->side);
+  if (e->side) (void)hipStreamSynchronize(e->side);
   e->timer.clear();
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
@@ -298,9 +297,11 @@ int hbh_engine_destroy(hbh_engine* e) {
     b->release();
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   (void)hipEventDestroy(e->done);
-  (void)hipEventDestroy(e->fork);
-  (void)hipEventDestroy(e->join);
-  (void)hipStreamDestroy(e->side);
+  if (e->side) {
+    (void)hipEventDestroy(e->fork);
+    (void)hipEventDestroy(e->join);
+    (void)hipStreamDestroy(e->side);
+  }
   for (hipEvent_t ev : e->slot_done)
     if (ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
@@ -793,7 +794,8 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
 // latency case).  e(g1, sigma) == e(mpk, H) with sigma = sum_k lambda_k sigma_k is, by bilinearity,
 //   prod_k e(lambda_k g1, sigma_k) * e(-mpk, H) == 1,
 // which needs no sigma: its m + 1 Miller loops (two pairs per wave, k_wave's Miller-only mode) run on a
-// second stream WHILE the engine stream interpolates sigma, and one wave per combine multiplies the
+// second stream WHILE the engine stream interpolates sigma (one pair per wave, homogeneous walk: mode
+// W1J of tools/gen_wave_prog.py), and one wave per combine multiplies the
 // partial values and runs the single final exponentiation (wave_prod_fe).  The verdict is the same
 // boolean for every input (an exact identity, no randomisation); lambda_k g1 comes from the device comb
 // table summed in a 5-level tree on lane quads (k_g1_gen_quad) on the side stream, left in Jacobian
@@ -802,6 +804,9 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
 #ifndef HBH_SPLIT_CHECK_MAX
 #define HBH_SPLIT_CHECK_MAX 8
 #endif
+#ifndef HBH_SPLIT_PAIRS
+#define HBH_SPLIT_PAIRS 1
+#endif
 }  // namespace
 extern "C" int hbh__host_g1_neg(const uint8_t* pk, uint8_t* neg_out);
 namespace {
@@ -809,7 +814,10 @@ namespace {
 int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vector<uint32_t>& xs,
                          const uint8_t* shares, const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out,
                          int* status, uint8_t* verdicts) {
-  const size_t np = m + 1, nw = (np + 1) / 2, nchk = ncomb * nw, nq = ncomb * np;
+  // SPLIT_PAIRS pairs per wave: 1 = the homogeneous-walk program (two stages per Miller step),
+  // 2 = the two-sided Jacobian program (WWJ, three stages per step, half the waves)
+  constexpr int pairs = HBH_SPLIT_PAIRS;
+  const size_t np = m + 1, nw = (np + pairs - 1) / pairs, nchk = ncomb * nw, nq = ncomb * np;
   constexpr size_t JB = 3 * 48;  // Jacobian P: X || Y || Z canonical
   uint8_t negpk[HBH_G1_BYTES];
   if (hbh__host_g1_neg(master_pk, negpk)) return fail(HBH_ERR_ARG, "master key coordinate >= p");
@@ -822,6 +830,11 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   const size_t o_v = ncomb * HBH_G2_BYTES, out_bytes = o_v + ncomb;
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
+  if (!e->side) {
+    HBH_CHECK(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    HBH_CHECK(hipEventCreateWithFlags(&e->fork, hipEventDisableTiming));
+    HBH_CHECK(hipEventCreateWithFlags(&e->join, hipEventDisableTiming));
+  }
   const size_t stage_bytes = std::max(in_bytes, out_bytes);
   if (stage_bytes > e->h_stage_cap) {
     if (e->h_stage) HBH_CHECK(hipHostFree(e->h_stage));
@@ -841,8 +854,8 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   uint32_t* i1 = (uint32_t*)(hs + o_i1);
   for (size_t c = 0; c < ncomb; c++)
     for (size_t w = 0; w < nw; w++)
-      for (int sd = 0; sd < 2; sd++) {
-        const size_t k = 2 * w + sd, j = c * nw + w;
+      for (int sd = 0; sd < pairs; sd++) {
+        const size_t k = pairs * w + sd, j = c * nw + w;
         uint32_t* qi = sd ? &i1[j] : &i0[j];
         if (k < m) {
           *qi = (uint32_t)(c * m + k);  // (lambda_k g1, sigma_k): P written by k_g1_gen_quad
@@ -873,12 +886,13 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   // and the final exponentiation
   int rc = ensure_fbtab(e, s2);
   if (rc) return rc;
-  HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, e->fbtab.p, (const uint32_t*)(din + o_lam),
+  HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, pairs, e->fbtab.p, (const uint32_t*)(din + o_lam),
                              din + o_p0, din + o_p1));
   hbl::PairSideDesc sd0 = {din + o_p0, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i0), nq};
   hbl::PairSideDesc sd1 = {din + o_p1, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i1), nq};
   hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
-  HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1, hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P, nullptr,
+  HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1,
+                             hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P | (pairs == 1 ? hbl::WAVE_ONE_SIDE : 0), nullptr,
                              (uint32_t*)e->fval.p));
   HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, dout + o_v));
   e->timer.end(s2, tp);

@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(64) k_interp_g1_join(int ncomb, const int32_t*
 // operations of 5 product rounds each instead of 32 sequential additions); quad 0 writes the Jacobian
 // sum (no inversion) as point p = (c, k) of combine c to side k & 1 of wave c * nw + k / 2 -- the P
 // arrays the Miller-only k_wave launch reads (WAVE_JAC_P).
-__global__ void __launch_bounds__(64) k_g1_gen_quad(int n, int m, int nw, const uint32_t* __restrict__ tab,
+__global__ void __launch_bounds__(64) k_g1_gen_quad(int n, int m, int nw, int pairs, const uint32_t* __restrict__ tab,
                                                     const uint32_t* __restrict__ scalars, uint32_t* __restrict__ out0,
                                                     uint32_t* __restrict__ out1) {
   __shared__ int32_t sm[16 * Q_JROW_WORDS];
@@ -410,7 +410,7 @@ __global__ void __launch_bounds__(64) k_g1_gen_quad(int n, int m, int nw, const 
   }
   if (g != 0) return;
   const int c = p / m, k = p % m;
-  uint32_t* o = ((k & 1) ? out1 : out0) + ((size_t)c * nw + k / 2) * 36;
+  uint32_t* o = pairs == 1 ? out0 + ((size_t)c * nw + k) * 36 : ((k & 1) ? out1 : out0) + ((size_t)c * nw + k / 2) * 36;
   if (qj_zero(acc)) {
     if (q_lane() == 0)
       for (int i = 0; i < 36; i++) o[i] = 0u;
@@ -426,11 +426,11 @@ __global__ void __launch_bounds__(64) k_g1_gen_quad(int n, int m, int nw, const 
 
 namespace hbl {
 
-hipError_t g1_gen_tree(hipStream_t s, int n, int m, int nw, const void* tab, const uint32_t* scalars, void* out0,
-                       void* out1) {
+hipError_t g1_gen_tree(hipStream_t s, int n, int m, int nw, int pairs, const void* tab, const uint32_t* scalars,
+                       void* out0, void* out1) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hbs::k_g1_gen_quad, dim3((unsigned)n), dim3(64), 0, s, n, m, nw, (const uint32_t*)tab, scalars,
-                     (uint32_t*)out0, (uint32_t*)out1);
+  hipLaunchKernelGGL(hbs::k_g1_gen_quad, dim3((unsigned)n), dim3(64), 0, s, n, m, nw, pairs, (const uint32_t*)tab,
+                     scalars, (uint32_t*)out0, (uint32_t*)out1);
   return hipGetLastError();
 }
 

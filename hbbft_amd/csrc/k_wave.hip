@@ -39,7 +39,7 @@ struct WaveArgs {
   int n;
   WaveSide s[2];
   int flags;            // bit 0: negate P2; bit 1: conjugated value (single pairing); bit 2: Miller only;
-                        // bit 3: Jacobian P (36 words, both sides WALK)
+                        // bit 3: Jacobian P (36 words, both sides WALK); bit 4 (with 3): side 0 only
   uint8_t* verdict;
   uint32_t* value_out;  // 144 canonical words per check (may be null)
   const uint32_t* fin;  // product mode: nf Miller values (144 words, w-basis) per check; null otherwise
@@ -509,6 +509,7 @@ HP_D const int4* wave_side(const WaveArgs& a, uint32_t* sm, int i, int h, int pa
 }
 
 // the constant slots of tools/gen_wave_prog.py CONSTS and F = 1 (pair k writes slot k)
+static_assert(hbw::WP_F == 18, "CONSTS of tools/gen_wave_prog.py: 18 constant slots before F");
 HP_D void wave_consts(uint32_t* sm, int h, int pair) {
   switch (pair) {
     case 0: put_const(sm, h, 0, WV_ZW, WV_ZW); break;
@@ -528,9 +529,14 @@ HP_D void wave_consts(uint32_t* sm, int h, int pair) {
     case 14: put_const(sm, h, 14, hb::G1X_M, WV_ZW); break;
     case 15: put_const(sm, h, 15, hb::G1Y_M, WV_ZW); break;
     case 16: put_const(sm, h, 16, hb::G1NY_M, WV_ZW); break;
-    case 17: put_const(sm, h, hbw::WP_F, hb::ONE_L, WV_ZW); break;
+    case 17: {  // 12 xi = 3 b' (both components 12), the homogeneous walk of mode W1J
+      const Fp six = fp_lin(6, fp_one(), 0, fp_one());
+      st_own(sm, 17, h, fp_reduce(fp_add(six, six)));
+      break;
+    }
+    case 18: put_const(sm, h, hbw::WP_F, hb::ONE_L, WV_ZW); break;
     default:
-      if (pair < 23) put_const(sm, h, hbw::WP_F + pair - 17, WV_ZW, WV_ZW);
+      if (pair < 24) put_const(sm, h, hbw::WP_F + pair - 18, WV_ZW, WV_ZW);
       break;
   }
 }
@@ -563,14 +569,16 @@ __global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
     // the two sides: P (G1) -> XP, YP as Fp2 (x, 0); Q -> QX, QY and T = (Q, 1); activity flags
     bool act0, act1, bad0, bad1;
     const int4* tl0 = wave_side<0>(a, sm, i, h, pair, act0, bad0);
-    const int4* tl1 = wave_side<1>(a, sm, i, h, pair, act1, bad1);
+    const int4* tl1 = nullptr;
+    act1 = bad1 = false;
+    if (!(a.flags & 16)) tl1 = wave_side<1>(a, sm, i, h, pair, act1, bad1);
     const bool bad = bad0 || bad1;
     if (bad) {  // index out of range: reject, never read past a table (uniform per workgroup)
       if (lane == 0 && a.verdict) a.verdict[i] = 0;
       return;
     }
     __syncthreads();
-    const int mv = (a.flags & 8) ? 4 : (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
+    const int mv = (a.flags & 16) ? 5 : (a.flags & 8) ? 4 : (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
     run_stages(sm, hbw::WP_MILLER_OFF[mv], hbw::WP_MILLER_N[mv], h, pair, act0, act1, tl0, tl1);
     if (a.flags & 4) {  // Miller only: f (w-basis) out, no final exponentiation
       if (pair < 6 && a.value_out)

@@ -45,6 +45,9 @@ constexpr int WAVE_MILLER_ONLY = 4;
 // flags bit 3 (WAVE_JAC_P): every P is Jacobian, X || Y || Z canonical (36 words, Z = 0 at infinity);
 // both sides must WALK.  The lines are scaled by Z^3, so no inversion of Z is needed.
 constexpr int WAVE_JAC_P = 8;
+// flags bit 4 (WAVE_ONE_SIDE, with WAVE_JAC_P): one pair per check, side 0 only (side 1 is not read):
+// the homogeneous-walk Miller program (two stages per step instead of three)
+constexpr int WAVE_ONE_SIDE = 16;
 hipError_t wave_prod_fe(hipStream_t s, int n, int nf, const uint32_t* fin, uint8_t* verdict);
 
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
@@ -81,10 +84,11 @@ size_t fb_table_bytes();
 hipError_t fb_table(hipStream_t s, void* tab);
 hipError_t g1_mul_gen(hipStream_t s, int n, const void* tab, const uint32_t* scalars, void* out);
 // lambda_k g1 (scalars 8 LE words each, n = ncomb * m) by a 5-level tree over the comb table, in
-// Jacobian form (36 words: X || Y || Z canonical, all zero at infinity) to out0 / out1 (even / odd k) at
-// wave c * nw + k / 2: the P sides of the split master check (k_wave with WAVE_JAC_P)
-hipError_t g1_gen_tree(hipStream_t s, int n, int m, int nw, const void* tab, const uint32_t* scalars, void* out0,
-                       void* out1);
+// Jacobian form (36 words: X || Y || Z canonical, all zero at infinity) to entry c * nw + k / 2 of out0 /
+// out1 (even / odd k; pairs = 2) or entry c * nw + k of out0 (pairs = 1): the P sides of the split master
+// check (k_wave with WAVE_JAC_P)
+hipError_t g1_gen_tree(hipStream_t s, int n, int m, int nw, int pairs, const void* tab, const uint32_t* scalars,
+                       void* out0, void* out1);
 // xs[k] = idx[k] + 1 for n = ncomb * m device-resident indices; status[k / m] = HBL_BAD_INDEX for
 // an index of 0xffffffff (status zeroed by the caller beforehand).
 hipError_t index_plus_one(hipStream_t s, int n, int m, const uint32_t* idx, uint32_t* xs, int* status);

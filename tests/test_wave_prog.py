@@ -53,11 +53,14 @@ def test_committed_include_is_current(progs, tmp_path):
 
 def test_program_shape(progs):
     for m, v in progs["variants"].items():
-        assert v["nstages_miller"] <= 215 and v["nstages_fe"] <= 360, m
+        assert v["nstages_miller"] <= 215 and v["nstages_fe"] <= 80, m
         assert progs["nslots"] <= 136
 
 
-@pytest.mark.parametrize("mode", W.MODES)
+TWO_SIDED = [m for m in W.MODES if m != "W1J"]  # W1J: one pair per wave (test_single_pair_homogeneous_walk)
+
+
+@pytest.mark.parametrize("mode", TWO_SIDED)
 def test_single_pairing_value(progs, mode):
     rnd = random.Random(7 + W.MODES.index(mode))
     Pp = C.g1_mul(C.G1_GEN, rnd.randrange(1, C.R))
@@ -66,7 +69,7 @@ def test_single_pairing_value(progs, mode):
     assert got == tower_to_w(cube(C.pairing(Pp, Q)))
 
 
-@pytest.mark.parametrize("mode", W.MODES)
+@pytest.mark.parametrize("mode", TWO_SIDED)
 def test_pairing_equality(progs, mode):
     rnd = random.Random(11 + W.MODES.index(mode))
     a, b = rnd.randrange(1, C.R), rnd.randrange(1, C.R)
@@ -138,3 +141,29 @@ def test_split_master_check_jacobian_p(progs):
     f = W.emulate_miller(vj, [(jac(P[0]), Q[0], False), (("JAC", (1, 1, 0)), Q[1], False)])
     g = W.emulate_miller(v, [(P[0], Q[0], False), (None, Q[1], False)])
     assert W.emulate_prod_fe(v, [f]) == W.emulate_prod_fe(v, [g])
+
+
+def test_single_pair_homogeneous_walk(progs):
+    """Mode W1J (one pair per wave, homogeneous-projective walk, Jacobian P): after the final
+    exponentiation the same value as the two-pair Jacobian walk with the second pair inactive, and the
+    split master check's product over one-pair waves is 1 exactly for a valid relation."""
+    rnd = random.Random(13)
+    v1, v = progs["variants"]["W1J"], progs["variants"]["WW"]
+    assert v1["nstages_miller"] <= 150
+
+    def jac(pt):
+        z = rnd.randrange(1, C.P)
+        return ("JAC", (pt[0] * z * z % C.P, pt[1] * z * z * z % C.P, z))
+
+    a, b = rnd.randrange(1, C.R), rnd.randrange(1, C.R)
+    Pp, Q = C.g1_mul(C.G1_GEN, a), C.g2_mul(C.G2_GEN, b)
+    got = W.emulate_prod_fe(v, [W.emulate_miller(v1, [(jac(Pp), Q, False)])])
+    want = W.emulate_prod_fe(v, [W.emulate_miller(v, [(Pp, Q, False), (None, Q, False)])])
+    assert got == want
+    assert W.emulate_prod_fe(v, [W.emulate_miller(v1, [(("JAC", (1, 1, 0)), Q, False)])]) == ONE_W
+    # e(a g1, b g2) e(-(ab) g1, g2) == 1 over two one-pair waves; off by one -> != 1
+    for k, want1 in ((a * b % C.R, True), ((a * b + 1) % C.R, False)):
+        m = C.g1_mul(C.G1_GEN, k)
+        fs = [W.emulate_miller(v1, [(jac(Pp), Q, False)]),
+              W.emulate_miller(v1, [(jac((m[0], (-m[1]) % C.P)), C.G2_GEN, False)])]
+        assert (W.emulate_prod_fe(v, fs) == ONE_W) == want1

@@ -36,7 +36,8 @@ SPECIAL_INV = 1
 SPECIAL_CYC = 2  # a run of cyclotomic squarings kept in registers (k_wave.hip cyc_run)
 
 # fixed slot map shared with the kernel prologue
-CONSTS = ["ZERO", "ONE"] + ["F1_%d" % k for k in range(6)] + ["F2_%d" % k for k in range(6)] + ["G1X", "G1Y", "G1NY"]
+CONSTS = (["ZERO", "ONE"] + ["F1_%d" % k for k in range(6)] + ["F2_%d" % k for k in range(6)] + ["G1X", "G1Y", "G1NY"]
+          + ["K12XI"])  # 12 xi = 3 b' (the homogeneous walk of mode W1J)
 SIDE_FIELDS = ["XP", "YP", "QX", "QY", "TX", "TY", "TZ", "ZP"]  # ZP: Z^3 of a Jacobian P (mode WWJ)
 MULF_G = ["S0_" + f for f in SIDE_FIELDS[:6]]
 
@@ -354,6 +355,72 @@ class Builder:
                 self.add(op_sqr12(self.F, self.F))
             for side in (0, 1):
                 self.add(op_mul_line(self.F, self.F, L(side, s)))
+
+    # ---- Miller loop of ONE pair (mode W1J: the split master check, one pair per wave)
+    def miller1(self):
+        """Side 0 only, WALK, Jacobian P (XP = X Z, YP = Y, ZP = Z^3 as in WWJ).  T is kept in
+        HOMOGENEOUS projective coordinates (x = X/Z, y = Y/Z) with Zk = 12 xi Z = 3 b' Z carried along,
+        so a doubling is two product levels instead of three (Costello-Lange-Naehrig / Aranha et al.
+        2011 formulas for a = 0, scaled by -4 to clear the halves):
+          X3 = -2 XY (B - 3 E), Y3 = 12 E^2 - (B + 3 E)^2, Z3 = -8 B YZ, Zk3 = -8 B (Y Zk)
+          (B = Y^2, E = Z Zk = 3 b' Z^2), line (c0, c1, c4) = (B - E, -3 X^2, 2 YZ);
+        a mixed addition is four levels (theta = Y - yQ Z, lambda = X - xQ Z; line (theta xQ - lambda
+        yQ, -theta, lambda)).  These lines are pairing 0.14's times Fp2 factors, which the final
+        exponentiation removes, and with one pair the f update (square, then one sparse line) is two
+        stages per step like the walk: ~145 stages instead of 211."""
+        steps = []
+        for b in range(62, -1, -1):
+            steps.append("D")
+            if (X_ABS >> b) & 1:
+                steps.append("A")
+        XP, YP, ZP, QX, QY, TX, TY, TZ = ("S0_" + f for f in ("XP", "YP", "ZP", "QX", "QY", "TX", "TY", "TZ"))
+        ZK = "W0_ZK"
+        T = lambda n: "W0_" + n
+        L = lambda s: ["L0_%d_%d" % (s % 2, c) for c in range(3)]
+        self.add(Op("NONE", [], [Out(ZK, [("K12XI", 1, 0)])], name="zk0"))  # Z = 1
+
+        def walk(s):
+            l = L(s)
+            if steps[s] == "D":
+                self.add(Op("M1", [[Prod(TX, TX)], [Prod(TY, TY)], [Prod(TZ, ZK)], [Prod(TX, TY)], [Prod(TY, TZ)],
+                                   [Prod(TY, ZK)]],
+                            [Out(T("LC1"), [(P_(0), -3, 0)]), Out(T("B"), [(P_(1), 1, 0)]),
+                             Out(T("BFM"), [(P_(1), 1, 0), (P_(2), -3, 0)]), Out(T("BFP"), [(P_(1), 1, 0), (P_(2), 3, 0)]),
+                             Out(T("E2"), [(P_(2), 2, 0)]), Out(T("E6"), [(P_(2), 6, 0)]), Out(T("XY"), [(P_(3), 1, 0)]),
+                             Out(T("YZ"), [(P_(4), 1, 0)]), Out(T("LC4"), [(P_(4), 2, 0)]), Out(T("YZK"), [(P_(5), 1, 0)]),
+                             Out(T("L0R"), [(P_(1), 1, 0), (P_(2), -1, 0)])], name="hdbl1"))
+                self.add(Op("M1", [[Prod(T("XY"), T("BFM"))], [Prod(T("BFP"), T("BFP"))], [Prod(T("E2"), T("E6"))],
+                                   [Prod(T("B"), T("YZ"))], [Prod(T("B"), T("YZK"))], [Prod(T("LC1"), XP)],
+                                   [Prod(T("LC4"), YP)], [Prod(T("L0R"), ZP)]],
+                            [Out(TX, [(P_(0), -2, 0)]), Out(TY, [(P_(2), 1, 0), (P_(1), -1, 0)]),
+                             Out(TZ, [(P_(3), -8, 0)]), Out(ZK, [(P_(4), -8, 0)]),
+                             Out(l[1], [(P_(5), 1, 0)], gate=0), Out(l[2], [(P_(6), 1, 0)], gate=0),
+                             Out(l[0], [(P_(7), 1, 0)], gate=0, default="ONE")], name="hdbl2"))
+            else:
+                self.add(Op("M1", [[Prod(QY, TZ)], [Prod(QX, TZ)]],
+                            [Out(T("TH"), [(TY, 1, 0), (P_(0), -1, 0)]), Out(T("LA"), [(TX, 1, 0), (P_(1), -1, 0)])],
+                            name="hadd1"))
+                self.add(Op("M1", [[Prod(T("TH"), T("TH"))], [Prod(T("LA"), T("LA"))], [Prod(T("TH"), QX)],
+                                   [Prod(T("LA"), QY)], [Prod(T("TH"), XP)], [Prod(T("LA"), YP)]],
+                            [Out(T("C"), [(P_(0), 1, 0)]), Out(T("D"), [(P_(1), 1, 0)]),
+                             Out(T("L0R"), [(P_(2), 1, 0), (P_(3), -1, 0)]),
+                             Out(l[1], [(P_(4), -1, 0)], gate=0), Out(l[2], [(P_(5), 1, 0)], gate=0)], name="hadd2"))
+                self.add(Op("M1", [[Prod(T("LA"), T("D"))], [Prod(TZ, T("C"))], [Prod(TX, T("D"))], [Prod(T("L0R"), ZP)]],
+                            [Out(T("E"), [(P_(0), 1, 0)]), Out(T("G"), [(P_(2), 1, 0)]),
+                             Out(T("H"), [(P_(0), 1, 0), (P_(1), 1, 0), (P_(2), -2, 0)]),
+                             Out(l[0], [(P_(3), 1, 0)], gate=0, default="ONE")], name="hadd3"))
+                self.add(Op("M1", [[Prod(T("LA"), T("H"))], [Prod(T("TH"), T("G"), d=T("H"), sd=-1)], [Prod(TY, T("E"))],
+                                   [Prod(TZ, T("E"))], [Prod(ZK, T("E"))]],
+                            [Out(TX, [(P_(0), 1, 0)]), Out(TY, [(P_(1), 1, 0), (P_(2), -1, 0)]),
+                             Out(TZ, [(P_(3), 1, 0)]), Out(ZK, [(P_(4), 1, 0)])], name="hadd4"))
+
+        walk(0)
+        for s, typ in enumerate(steps):
+            if s + 1 < len(steps):
+                walk(s + 1)
+            if typ == "D" and s > 0:
+                self.add(op_sqr12(self.F, self.F))
+            self.add(op_mul_line(self.F, self.F, L(s)))
 
     # ---- final exponentiation (k_pair.hip h_final_exp, the chain of pairing.hpp final_exp_x3)
     def final_exp(self):
@@ -674,6 +741,7 @@ def const_values():
     g1x = 0x17F1D3A73197D7942695638C4FA9AC0FC3688C4F9774B905A14E3A3F171BAC586C55E83FF97A1AEFFB3AF00ADB22C6BB
     g1y = 0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC744A2888AE40CAA232946C5E7E1
     v["G1X"], v["G1Y"], v["G1NY"] = (g1x, 0), (g1y, 0), ((-g1y) % P, 0)
+    v["K12XI"] = (12, 12)
     return v
 
 
@@ -872,7 +940,7 @@ def emulate_prod_fe(prog, fs):
 
 
 # ------------------------------------------------------------------------------- build / emit
-MODES = ["WW", "WT", "TW", "TT", "WWJ"]
+MODES = ["WW", "WT", "TW", "TT", "WWJ", "W1J"]
 
 
 def allocate(b, stages):
@@ -930,7 +998,10 @@ def build():
     nslots = max(fe.slots.values()) + 1
     for m in MODES:
         b = Builder(m)
-        b.miller(tuple(m))
+        if m == "W1J":
+            b.miller1()
+        else:
+            b.miller(tuple(m))
         st = schedule(b.ops)
         b.slots = allocate(b, st)
         nslots = max(nslots, max(b.slots.values()) + 1)
@@ -988,9 +1059,10 @@ def emit(out, path):
     lines.append("// F <- F * G with G in side 0's slots XP YP QX QY TX TY (product of partial Miller values)")
     lines.append("constexpr int WP_MULF_OFF = %d, WP_MULF_N = %d;" % (mf_off, mf_n))
     lines.append("// Miller programs: WALK/TABLE for side 0 and side 1 -> index (side0 is TABLE) * 2 + (side1 is TABLE);")
-    lines.append("// index 4: both sides WALK with Jacobian P (XP = X Z, YP = Y, ZP = Z^3)")
-    lines.append("constexpr int WP_MILLER_OFF[5] = {%s};" % ", ".join(str(i[0]) for i in info))
-    lines.append("constexpr int WP_MILLER_N[5] = {%s};" % ", ".join(str(i[1]) for i in info))
+    lines.append("// index 4: both sides WALK with Jacobian P (XP = X Z, YP = Y, ZP = Z^3); 5: side 0 only, the same")
+    lines.append("// Jacobian P, homogeneous walk (one pair per wave)")
+    lines.append("constexpr int WP_MILLER_OFF[6] = {%s};" % ", ".join(str(i[0]) for i in info))
+    lines.append("constexpr int WP_MILLER_N[6] = {%s};" % ", ".join(str(i[1]) for i in info))
 
     def arr(name, typ, vals, per):
         lines.append("__device__ __attribute__((aligned(16))) const %s %s[%d] = {" % (typ, name, len(vals)))
