@@ -296,8 +296,8 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
  *   HBH_IMPL_WAVE (k_wave.hip): one 64-lane wave per check; the check's Fp2 products run on 32 lane
  *     pairs side by side.  Latency path (one check: the master check of combine_and_verify_sig).
  *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, PAIR above (the
- *     measured crossover, profiles/r03/crossover_wave_pair.txt: 8,192 checks 11.6 vs 13.0 ms,
- *     12,288 checks 17.2 vs 13.1 ms).
+ *     measured crossover with the CYC-run final exponentiation, profiles/r03/crossover_wave_pair_cyc.txt:
+ *     8,192 checks 10.3 vs 12.4 ms, 12,288 checks 15.2 vs 12.5 ms; WAVE grows 1.24 ms per 1,024 checks).
  * Retired (selecting them returns HBH_ERR_ARG): HBH_IMPL_THREAD (0, round 1's one-thread kernel),
  * HBH_IMPL_LANE_COOP (1, six lanes per check) and HBH_IMPL_THREAD_SIGNED (2, one thread per check
  * on signed limbs) -- WAVE and PAIR cover every batch size faster. */
@@ -307,7 +307,7 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_AUTO 3
 #define HBH_IMPL_PAIR 4
 #define HBH_IMPL_WAVE 5
-#define HBH_AUTO_WAVE_MAX 8192
+#define HBH_AUTO_WAVE_MAX 9728
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 /* Ack-check kernel of hbh_bivar_ack_check_set: HBH_ACK_QUAD (k_bivar_check_quad: four lanes per ack
  * split each G1 operation, Jacobian rows -- latency), HBH_ACK_LANE (k_bivar_check: one lane per ack,

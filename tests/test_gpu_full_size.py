@@ -72,10 +72,10 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
 
 
 def test_config1_wave_at_auto_threshold(engine, sign_batch):
-    """Both kernels at the AUTO boundary (HBH_AUTO_WAVE_MAX = 8,192 checks: 128 documents of
+    """Both kernels at the AUTO boundary (HBH_AUTO_WAVE_MAX = 9,728 checks: 152 documents of
     configs[1]): WAVE walks both G2 sides, PAIR reads H's line table; verdicts equal the construction."""
     b = sign_batch
-    n = 8192
+    n = 9728
     from hbbft_amd._lib import IMPL_PAIR
     for impl in (IMPL_WAVE, IMPL_PAIR, IMPL_AUTO):
         engine.set_pairing_impl(impl)
