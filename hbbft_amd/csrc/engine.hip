@@ -83,6 +83,9 @@ struct StageTimer {
   }
 };
 
+#ifndef HBH_SPLIT_CHECK_MAX
+#define HBH_SPLIT_CHECK_MAX 8
+#endif
 struct hbh_engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -121,6 +124,7 @@ struct hbh_engine {
   uint8_t* h_stage = nullptr;  // pinned host staging of the split check (one upload, one download)
   size_t h_stage_cap = 0;
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
+  size_t split_max = HBH_SPLIT_CHECK_MAX;  // most combines per call on the split check (HBH_SPLIT_MAX)
 };
 
 namespace {
@@ -265,6 +269,7 @@ int hbh_engine_create(int device, hbh_engine** out) {
   hbh_engine* e = new hbh_engine();
   e->device = device;
   if (const char* v = std::getenv("HBH_SPLIT_CHECK")) e->split_check = std::atoi(v) != 0;
+  if (const char* v = std::getenv("HBH_SPLIT_MAX")) e->split_max = (size_t)std::max(0, std::atoi(v));
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
   if (err == hipSuccess) err = hipEventRecord(e->done, e->stream);
@@ -801,9 +806,6 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
 // table summed in a 5-level tree on lane quads (k_g1_gen_quad) on the side stream, left in Jacobian
 // form: the Miller kernel scales each line by Z^3 instead of inverting Z (WAVE_JAC_P).  A repeated index gives zero
 // lambdas (status DuplicateEntry), as in the interpolation.
-#ifndef HBH_SPLIT_CHECK_MAX
-#define HBH_SPLIT_CHECK_MAX 8
-#endif
 #ifndef HBH_SPLIT_PAIRS
 #define HBH_SPLIT_PAIRS 1
 #endif
@@ -950,7 +952,7 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
     if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
     xs[k] = idx[k] + 1;
   }
-  if (ncomb <= HBH_SPLIT_CHECK_MAX && e->split_check && hbl::interp_g2_pair_fits((int)m))
+  if (ncomb <= e->split_max && e->split_check && hbl::interp_g2_pair_fits((int)m))
     return combine_verify_split(e, ncomb, m, xs, shares, master_pk, hashes, out, status, verdicts);
   // P1 = master pk (one record per combine), P2 = the G1 generator (a flag, nothing uploaded)
   std::vector<uint8_t> p12(ncomb * HBH_G1_BYTES);
