@@ -83,8 +83,12 @@ struct StageTimer {
   }
 };
 
-#ifndef HBH_SPLIT_CHECK_MAX
-#define HBH_SPLIT_CHECK_MAX 8
+// split master check when the call has at most HBH_SPLIT_WAVES_MAX one-pair Miller waves (ncomb x (t + 2)):
+// measured crossover vs interpolate-then-verify (profiles/r03/split_sweep.jsonl) at ~45 combines for
+// t = 21 (~1,000 waves) and ~40 for t = 33 (~1,400 waves); HBH_SPLIT_MAX=<combines> in the environment
+// replaces the rule by a plain combine count (A/B)
+#ifndef HBH_SPLIT_WAVES_MAX
+#define HBH_SPLIT_WAVES_MAX 1280
 #endif
 struct hbh_engine {
   int device = 0;
@@ -124,7 +128,7 @@ struct hbh_engine {
   uint8_t* h_stage = nullptr;  // pinned host staging of the split check (one upload, one download)
   size_t h_stage_cap = 0;
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
-  size_t split_max = HBH_SPLIT_CHECK_MAX;  // most combines per call on the split check (HBH_SPLIT_MAX)
+  size_t split_max = 0;  // HBH_SPLIT_MAX: most combines per call on the split check (0: the wave rule)
 };
 
 namespace {
@@ -952,7 +956,8 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
     if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
     xs[k] = idx[k] + 1;
   }
-  if (ncomb <= e->split_max && e->split_check && hbl::interp_g2_pair_fits((int)m))
+  if (e->split_check && (e->split_max ? ncomb <= e->split_max : ncomb * (m + 1) <= HBH_SPLIT_WAVES_MAX) &&
+      ncomb <= INTERP_PAIR_MAX && hbl::interp_g2_pair_fits((int)m))
     return combine_verify_split(e, ncomb, m, xs, shares, master_pk, hashes, out, status, verdicts);
   // P1 = master pk (one record per combine), P2 = the G1 generator (a flag, nothing uploaded)
   std::vector<uint8_t> p12(ncomb * HBH_G1_BYTES);

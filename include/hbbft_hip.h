@@ -170,8 +170,8 @@ int hbh_interpolate_g1(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx
  * verdict[c] = PublicKey::verify_g2(out[c], hashes[c]) = (e(master_pk, H_c) == e(g1, out[c]))
  * (:260-266) without a host round trip in between.  status[c] as hbh_interpolate_g2; verdict[c]
  * = 0 is the reference's Error::VerificationFailed; verdicts of a combine whose status is not
- * HBH_OK are meaningless (the reference returns the combine error first).  Up to 8 combines per
- * call evaluate the same verdict as prod_k e(lambda_k g1, share_k) * e(-master_pk, H_c) == 1 on a
+ * HBH_OK are meaningless (the reference returns the combine error first).  Calls of at most 1,280
+ * one-pair Miller waves (ncomb x (t + 2); at most 384 combines) evaluate the same verdict as prod_k e(lambda_k g1, share_k) * e(-master_pk, H_c) == 1 on a
  * second stream while the first interpolates ("split master check"; the environment
  * variable HBH_SPLIT_CHECK=0 at engine creation selects interpolate-then-verify for every size). */
 int hbh_combine_verify_g2(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx, const uint8_t* shares,

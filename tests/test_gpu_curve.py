@@ -133,11 +133,30 @@ def test_combine_verify_g2_matches_two_step(engine):
     assert out[0] == g2a(bytes.fromhex(doc["combined_uncompressed"]))
 
 
+@pytest.fixture(scope="module")
+def unsplit_engine():
+    """An engine created with HBH_SPLIT_CHECK=0: every combine_and_verify_sig call interpolates, then
+    verifies (the engine reads the switch at creation)."""
+    from hbbft_amd.engine import Engine
+    old = os.environ.get("HBH_SPLIT_CHECK")
+    os.environ["HBH_SPLIT_CHECK"] = "0"
+    try:
+        e = Engine(0)
+    finally:
+        if old is None:
+            del os.environ["HBH_SPLIT_CHECK"]
+        else:
+            os.environ["HBH_SPLIT_CHECK"] = old
+    yield e
+    e.close()
+
+
 @pytest.mark.parametrize("t", [0, 1, 21, 70])
-def test_combine_verify_split_matches_unsplit(engine, t):
-    """Up to 8 combines per call take the split master check (partial Miller loops of (lambda_k g1,
-    sigma_k) and (-mpk, H) beside the interpolation, one final exponentiation per combine); 9 and more
-    the interpolate-then-verify form.  Same signatures, statuses and verdicts on the same inputs:
+def test_combine_verify_split_matches_unsplit(engine, unsplit_engine, t):
+    """Calls of at most 1,280 one-pair Miller waves (ncomb x (t + 2)) take the split master check
+    (partial Miller loops of (lambda_k g1, sigma_k) and (-mpk, H) beside the interpolation, one final
+    exponentiation per combine); larger calls, and an engine created with HBH_SPLIT_CHECK=0, the
+    interpolate-then-verify form.  Same signatures, statuses and verdicts on the same inputs:
     valid, wrong document, a tampered share (random G2 point), a share at infinity, a duplicate index."""
     rng = random.Random(700 + t)
     coeffs = [rng.randrange(1, C.R) for _ in range(t + 1)]
@@ -162,7 +181,8 @@ def test_combine_verify_split_matches_unsplit(engine, t):
         idx.append(sub)
         pts.append(row)
         hashes.append(h)
-    out9, st9, v9 = engine.combine_verify_g2(t, idx, pts, mpk, hashes)
+    out9, st9, v9 = unsplit_engine.combine_verify_g2(t, idx, pts, mpk, hashes)
+    assert engine.combine_verify_g2(t, idx, pts, mpk, hashes) == (out9, st9, v9)
     out8, st8, v8 = engine.combine_verify_g2(t, idx[:8], pts[:8], mpk, hashes[:8])
     out1, st1, v1 = engine.combine_verify_g2(t, idx[:1], pts[:1], mpk, hashes[:1])
     assert (out8, st8, v8) == (out9[:8], st9[:8], v9[:8])

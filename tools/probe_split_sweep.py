@@ -29,7 +29,7 @@ def pe(x):
 
 
 n = 3 * t + 1
-modes = {"split": ("1", "100000"), "unsplit": ("0", "0")}
+modes = {"split": ("1", "100000"), "unsplit": ("0", "0"), "auto": ("1", "0")}
 engines = {}
 for name, (chk, mx) in modes.items():
     os.environ["HBH_SPLIT_CHECK"], os.environ["HBH_SPLIT_MAX"] = chk, mx
@@ -57,5 +57,5 @@ for nc in sizes:
             ts.append((time.perf_counter() - t0) * 1e3)
         res[name + "_ms"] = round(statistics.median(ts), 3)
         assert list(outs[name][1]) == [0] * nc and bytes(outs[name][2]) == b"\x01" * nc, name
-    assert outs["split"] == outs["unsplit"]
+    assert outs["split"] == outs["unsplit"] == outs["auto"]
     print(json.dumps(res), flush=True)
