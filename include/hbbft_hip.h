@@ -173,7 +173,8 @@ int hbh_interpolate_g1(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx
  * HBH_OK are meaningless (the reference returns the combine error first).  Calls of at most 1,280
  * one-pair Miller waves (ncomb x (t + 2); at most 384 combines) evaluate the same verdict as prod_k e(lambda_k g1, share_k) * e(-master_pk, H_c) == 1 on a
  * second stream while the first interpolates ("split master check"; the environment
- * variable HBH_SPLIT_CHECK=0 at engine creation selects interpolate-then-verify for every size). */
+ * variable HBH_SPLIT_CHECK=0 at engine creation selects interpolate-then-verify for every size;
+ * HBH_SPLIT_MAX=<n> replaces the wave-count rule by "at most n combines per call"). */
 int hbh_combine_verify_g2(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx, const uint8_t* shares,
                           const uint8_t* master_pk, const uint8_t* hashes, uint8_t* out, int* status,
                           uint8_t* verdicts);
