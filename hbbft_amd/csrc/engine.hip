@@ -10,6 +10,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/hbbft_hip.h"
@@ -83,13 +84,14 @@ struct StageTimer {
   }
 };
 
-// split master check when the call has at most HBH_SPLIT_WAVES_MAX one-pair Miller waves (ncomb x (t + 2)):
-// measured crossover vs interpolate-then-verify (profiles/r03/split_sweep.jsonl) at ~45 combines for
-// t = 21 (~1,000 waves) and ~40 for t = 33 (~1,400 waves); HBH_SPLIT_MAX=<combines> in the environment
-// replaces the rule by a plain combine count (A/B)
-#ifndef HBH_SPLIT_WAVES_MAX
-#define HBH_SPLIT_WAVES_MAX 1280
-#endif
+// split master check when the call has at most split_waves_max(t) one-pair Miller waves
+// (ncomb x (t + 2)).  Crossover against interpolate-then-verify, interpolated linearly between the
+// measured batch sizes of profiles/r03/split_sweep_auto.jsonl: t = 21 at ~45 combines (~1,046 waves;
+// 32 combines split 2.81 vs 3.60 ms, 48 combines 3.80 vs 3.70 ms), t = 33 at ~38 combines (~1,340
+// waves; 33 combines 4.26 vs 4.66 ms, 40 combines 4.75 vs 4.59 ms).  One wave cap cannot fit both
+// (ADVICE r3), so the cap grows with t through those two points: 540 + 24 t.
+// HBH_SPLIT_MAX=<combines> in the environment replaces the rule by a plain combine count (A/B).
+inline size_t split_waves_max(int t) { return 540 + 24 * (size_t)t; }
 struct hbh_engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -129,7 +131,11 @@ struct hbh_engine {
   size_t h_stage_cap = 0;
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
   size_t split_max = 0;  // HBH_SPLIT_MAX: most combines per call on the split check (0: the wave rule)
+  // commitment sets created on this engine: hbh_engine_destroy frees their device memory and
+  // detaches them, so a set destroyed after its engine never touches the freed engine
+  std::unordered_set<hbh_commit_set*> sets;
 };
+void release_set_device(hbh_commit_set* cs);
 
 namespace {
 
@@ -293,6 +299,13 @@ int hbh_engine_create(int device, hbh_engine** out) {
 int hbh_engine_destroy(hbh_engine* e) {
   if (!e) return HBH_OK;
   (void)hipSetDevice(e->device);
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipEventSynchronize(e->done);
+    (void)hipStreamSynchronize(e->stream);
+    for (hbh_commit_set* cs : e->sets) release_set_device(cs);  // detaches cs from e
+    e->sets.clear();
+  }
   (void)hipEventSynchronize(e->done);
   for (hipEvent_t ev : e->slot_done)
     if (ev) (void)hipEventSynchronize(ev);
@@ -826,7 +839,7 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   const size_t np = m + 1, nw = (np + pairs - 1) / pairs, nchk = ncomb * nw, nq = ncomb * np;
   constexpr size_t JB = 3 * 48;  // Jacobian P: X || Y || Z canonical
   uint8_t negpk[HBH_G1_BYTES];
-  if (hbh__host_g1_neg(master_pk, negpk)) return fail(HBH_ERR_ARG, "master key coordinate >= p");
+  if (hbh__host_g1_neg(master_pk, negpk)) return fail(HBH_ERR_ARG, "master key coordinate >= p");  // checked by the caller too
   bool pk_inf = true;
   for (int b = 0; b < HBH_G1_BYTES; b++) pk_inf = pk_inf && negpk[b] == 0;
   // one upload: Q table (shares, then one H per combine) | GLS digits | lambdas | P sides | Q indices
@@ -888,29 +901,41 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
   HBH_CHECK(hipMemcpyAsync(din, hs, in_bytes, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipEventRecord(e->fork, s));
   HBH_CHECK(hipStreamWaitEvent(s2, e->fork, 0));
-  // side stream: lambda_k g1 (Jacobian, over the zero P entries), the m + 1 Miller loops, the product
-  // and the final exponentiation
-  int rc = ensure_fbtab(e, s2);
-  if (rc) return rc;
-  HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, pairs, e->fbtab.p, (const uint32_t*)(din + o_lam),
-                             din + o_p0, din + o_p1));
-  hbl::PairSideDesc sd0 = {din + o_p0, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i0), nq};
-  hbl::PairSideDesc sd1 = {din + o_p1, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i1), nq};
-  hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
-  HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1,
-                             hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P | (pairs == 1 ? hbl::WAVE_ONE_SIDE : 0), nullptr,
-                             (uint32_t*)e->fval.p));
-  HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, dout + o_v));
-  e->timer.end(s2, tp);
-  // engine stream, concurrently: the interpolation (lane-quad latency form, host digits)
-  hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)(din + o_dg), din + o_q, e->ipart.p, dout));
-  e->timer.end(s, tm);
-  HBH_CHECK(hipEventRecord(e->join, s2));
-  HBH_CHECK(hipStreamWaitEvent(s, e->join, 0));
-  HBH_CHECK(hipMemcpyAsync(hs, dout, out_bytes, hipMemcpyDeviceToHost, s));
+  // From here on both streams hold queued work: every exit joins the side stream into s and closes the
+  // call on s, so e->done covers the side stream's kernels even when a launch fails.
+  auto launch = [&]() -> int {
+    // side stream: lambda_k g1 (Jacobian, over the zero P entries), the m + 1 Miller loops, the product
+    // and the final exponentiation
+    int rc = ensure_fbtab(e, s2);
+    if (rc) return rc;
+    HBH_CHECK(hbl::g1_gen_tree(s2, (int)(ncomb * m), (int)m, (int)nw, pairs, e->fbtab.p,
+                               (const uint32_t*)(din + o_lam), din + o_p0, din + o_p1));
+    hbl::PairSideDesc sd0 = {din + o_p0, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i0), nq};
+    hbl::PairSideDesc sd1 = {din + o_p1, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i1), nq};
+    hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
+    HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1,
+                               hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P | (pairs == 1 ? hbl::WAVE_ONE_SIDE : 0),
+                               nullptr, (uint32_t*)e->fval.p));
+    HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, dout + o_v));
+    e->timer.end(s2, tp);
+    // engine stream, concurrently: the interpolation (lane-quad latency form, host digits)
+    hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
+    HBH_CHECK(hbl::interp_g2_pair(s, (int)ncomb, (int)m, (const uint64_t*)(din + o_dg), din + o_q, e->ipart.p, dout));
+    e->timer.end(s, tm);
+    return HBH_OK;
+  };
+  const int lrc = launch();
+  const hipError_t jerr = hipEventRecord(e->join, s2);
+  const hipError_t werr = jerr == hipSuccess ? hipStreamWaitEvent(s, e->join, 0) : jerr;
+  if (werr != hipSuccess) {  // cannot order s after s2: drain both before the workspaces are reused
+    (void)hipStreamSynchronize(s2);
+    (void)hipStreamSynchronize(s);
+  }
+  if (!lrc && werr == hipSuccess) HBH_CHECK(hipMemcpyAsync(hs, dout, out_bytes, hipMemcpyDeviceToHost, s));
   {
     const int rc_ = end_call(e, s);
+    if (lrc) return lrc;
+    if (werr != hipSuccess) return fail(HBH_ERR_DEVICE, std::string("split check join: ") + hipGetErrorString(werr));
     if (rc_) return rc_;
   }
   HBH_CHECK(hipStreamSynchronize(s));
@@ -956,7 +981,13 @@ int hbh_combine_verify_g2(hbh_engine* e, size_t ncomb, int t, const uint32_t* id
     if (idx[k] == 0xffffffffu) return fail(HBH_ERR_ARG, "node index out of range");
     xs[k] = idx[k] + 1;
   }
-  if (e->split_check && (e->split_max ? ncomb <= e->split_max : ncomb * (m + 1) <= HBH_SPLIT_WAVES_MAX) &&
+  {
+    // one contract for both forms of the check: a master key coordinate >= p is an argument error
+    // (the split form rejected it, interpolate-then-verify returned verdicts)
+    uint8_t negpk[HBH_G1_BYTES];
+    if (hbh__host_g1_neg(master_pk, negpk)) return fail(HBH_ERR_ARG, "master key coordinate >= p");
+  }
+  if (e->split_check && (e->split_max ? ncomb <= e->split_max : ncomb * (m + 1) <= split_waves_max(t)) &&
       ncomb <= INTERP_PAIR_MAX && hbl::interp_g2_pair_fits((int)m))
     return combine_verify_split(e, ncomb, m, xs, shares, master_pk, hashes, out, status, verdicts);
   // P1 = master pk (one record per combine), P2 = the G1 generator (a flag, nothing uploaded)
@@ -1390,6 +1421,25 @@ struct hbh_commit_set {
   DevBuf stage;      // indices of rows computed by a call
 };
 
+// Frees a set's device memory and detaches it from its engine (cs->e = nullptr): every later call on
+// the set fails with HBH_ERR_ARG, and hbh_commit_set_destroy only deletes the host object.  Caller
+// holds the engine lock with the engine's streams drained.
+void release_set_device(hbh_commit_set* cs) {
+  if (cs->commits) (void)hipFree(cs->commits);
+  cs->commits = nullptr;
+  cs->commits_cap = 0;
+  cs->nparts = 0;
+  for (auto& R : cs->rows) {
+    if (R.p) (void)hipFree(R.p);
+    R.p = nullptr;
+    R.cap = 0;
+    R.n = 0;
+    R.slot.clear();
+  }
+  cs->stage.release();
+  cs->e = nullptr;
+}
+
 namespace {
 // Grow a device allocation to at least `want` bytes, keeping its first `used` bytes.
 int grow_keep(hipStream_t s, void** p, size_t* cap, size_t used, size_t want) {
@@ -1430,24 +1480,29 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, bool affine, size_t n, const uin
   if (np.empty()) return HBH_OK;
   const size_t row_bytes = affine ? (size_t)(cs->t + 1) * HBH_G1_BYTES : hbl::bivar_rows_quad_bytes(1, cs->t);
   const size_t first = R.n;
-  int rc = grow_keep(s, &R.p, &R.cap, first * row_bytes, (first + np.size()) * row_bytes);
-  if (rc) {
+  auto compute = [&]() -> int {
+    int rc = grow_keep(s, &R.p, &R.cap, first * row_bytes, (first + np.size()) * row_bytes);
+    if (rc) return rc;
+    HBH_CHECK(cs->stage.ensure(np.size() * 8));
+    uint32_t* d_p = (uint32_t*)cs->stage.p;
+    HBH_CHECK(hipMemcpyAsync(d_p, np.data(), np.size() * 4, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipMemcpyAsync(d_p + np.size(), nx.data(), nx.size() * 4, hipMemcpyHostToDevice, s));
+    hipEvent_t tm = cs->e->timer.begin(s, HBH_STAGE_CURVE, cs->e->profiling);
+    void* dst = (uint8_t*)R.p + first * row_bytes;
+    if (affine)
+      HBH_CHECK(hbl::bivar_row(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(), dst));
+    else
+      HBH_CHECK(hbl::bivar_row_quad(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(), dst));
+    cs->e->timer.end(s, tm);
+    // the staged indices are read by the kernel: the host vectors die at return
+    HBH_CHECK(hipStreamSynchronize(s));
+    return HBH_OK;
+  };
+  const int rc = compute();
+  if (rc) {  // the new slots were never filled: forget them, so no later ack reads an empty row
     for (size_t k = 0; k < np.size(); k++) R.slot.erase(((uint64_t)np[k] << 32) | nx[k]);
     return rc;
   }
-  HBH_CHECK(cs->stage.ensure(np.size() * 8));
-  uint32_t* d_p = (uint32_t*)cs->stage.p;
-  HBH_CHECK(hipMemcpyAsync(d_p, np.data(), np.size() * 4, hipMemcpyHostToDevice, s));
-  HBH_CHECK(hipMemcpyAsync(d_p + np.size(), nx.data(), nx.size() * 4, hipMemcpyHostToDevice, s));
-  hipEvent_t tm = cs->e->timer.begin(s, HBH_STAGE_CURVE, cs->e->profiling);
-  void* dst = (uint8_t*)R.p + first * row_bytes;
-  if (affine)
-    HBH_CHECK(hbl::bivar_row(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(), dst));
-  else
-    HBH_CHECK(hbl::bivar_row_quad(s, (int)np.size(), cs->t, cs->commits, d_p, d_p + np.size(), dst));
-  cs->e->timer.end(s, tm);
-  // the staged indices are read by the kernel: the host vectors die at return
-  HBH_CHECK(hipStreamSynchronize(s));
   R.n = first + np.size();
   return HBH_OK;
 }
@@ -1487,27 +1542,31 @@ int hbh_commit_set_create(hbh_engine* e, int t, hbh_commit_set** out) {
   cs->e = e;
   cs->t = t;
   cs->ncoef = (size_t)(t + 1) * (t + 2) / 2;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->sets.insert(cs);
+  }
   *out = cs;
   return HBH_OK;
 }
 
 int hbh_commit_set_destroy(hbh_commit_set* cs) {
   if (!cs) return HBH_OK;
-  hbh_engine* e = cs->e;
-  std::lock_guard<std::mutex> lk(e->mu);
-  (void)hipSetDevice(e->device);
-  (void)hipEventSynchronize(e->done);
-  (void)hipStreamSynchronize(e->stream);
-  if (cs->commits) (void)hipFree(cs->commits);
-  for (auto& R : cs->rows)
-    if (R.p) (void)hipFree(R.p);
-  cs->stage.release();
+  if (hbh_engine* e = cs->e) {  // else: detached by hbh_engine_destroy, device memory already freed
+    std::lock_guard<std::mutex> lk(e->mu);
+    (void)hipSetDevice(e->device);
+    (void)hipEventSynchronize(e->done);
+    (void)hipStreamSynchronize(e->stream);
+    e->sets.erase(cs);
+    release_set_device(cs);
+  }
   delete cs;
   return HBH_OK;
 }
 
 int hbh_commit_set_add(hbh_commit_set* cs, size_t nparts, const uint8_t* commits, size_t* first) {
   if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (!cs->e) return fail(HBH_ERR_ARG, "commitment set detached: its engine was destroyed");
   if (first) *first = cs->nparts;
   if (nparts == 0) return HBH_OK;
   if (!commits) return fail(HBH_ERR_ARG, "null pointer");
@@ -1538,6 +1597,7 @@ int hbh_commit_set_size(const hbh_commit_set* cs, size_t* nparts, size_t* nrows)
 
 int hbh_bivar_row_set(hbh_commit_set* cs, size_t nrow, const uint32_t* part_idx, const uint32_t* xs, uint8_t* out) {
   if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (!cs->e) return fail(HBH_ERR_ARG, "commitment set detached: its engine was destroyed");
   if (nrow == 0) return HBH_OK;
   if (!part_idx || !xs || !out) return fail(HBH_ERR_ARG, "null pointer");
   int rc = check_parts(cs, nrow, part_idx);
@@ -1568,6 +1628,7 @@ int hbh_bivar_row_set(hbh_commit_set* cs, size_t nrow, const uint32_t* part_idx,
 int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* part_idx, const uint32_t* xs,
                             const uint32_t* ys, const uint8_t* vals, uint8_t* verdicts) {
   if (!cs) return fail(HBH_ERR_ARG, "null commitment set");
+  if (!cs->e) return fail(HBH_ERR_ARG, "commitment set detached: its engine was destroyed");
   if (nack == 0) return HBH_OK;
   if (!part_idx || !xs || !ys || !vals || !verdicts) return fail(HBH_ERR_ARG, "null pointer");
   if (nack > ((size_t)1 << 28)) return fail(HBH_ERR_ARG, "batch too large");

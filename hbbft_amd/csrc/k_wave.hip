@@ -223,8 +223,7 @@ HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, boo
 // (f2, f5) -> (r1, r4), each of three Fp2 squares sA = A^2, sB = B^2, sAB = (A + B)^2 and outputs
 //   X = 3 (sA + xi sB) - 2 L,  Y = 3 (sAB - sA - sB) + 2 L,  Z = 3 xi (sAB - sA - sB) + 2 L
 // with L the input at the output's position.  Lane row g (16 lanes) runs one Fp4 squaring: lane quads
-// 0 / 1 hold A / B (own Fp2 component, both product halves), quad 2 squares A + B, each Fp product on
-// two lanes (fp_mul_split); the squares and the two inputs move by lane shuffles (ds_bpermute) inside
+// 0 / 1 hold A / B (own Fp2 component), quad 2 squares A + B; the squares and the two inputs move by lane shuffles (ds_bpermute) inside
 // the wave -- no LDS slot traffic and no barrier per squaring.  Row 0
 // keeps (f0, f3).  Rows 1 and 2 swap roles each squaring: the row squaring (f1, f4) produces the next
 // (f2, f5) and vice versa, so squaring inputs never move; only L crosses between rows 1 and 2.
@@ -249,60 +248,13 @@ HP_D Fp fp_red_3k(const Fp& t, const Fp& a, int k) {
   r.l[NL - 1] = (int32_t)(acc + top - (int64_t)q * (int32_t)P_L[NL - 1]);
   return r;
 }
-// x * y (Fp, fp_mul_l's contract) on TWO lanes: lane rr = 0 accumulates each column's x_i y_{k-i}
-// terms, lane rr = 1 the same column's m_i p_{k-i} reduction terms -- one MAD instruction does one term
-// of each, since both are sum_i A_i B_{k-i} over the same index range (A = x | m, B = y | p) -- and the
-// two partial column sums meet by DPP (quad_perm [2,3,0,1]) before the Montgomery digit.  210 MADs on
-// the critical path instead of 392; both lanes return the product.
-HP_D Fp fp_mul_split(const Fp& x, const Fp& y, bool rr) {
-  int32_t A[NL], B[NL];
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    A[i] = rr ? 0 : x.l[i];
-    B[i] = rr ? (int32_t)P_L[i] : y.l[i];
-  }
-  int64_t carry = 0;
-  Fp r;
-#pragma unroll
-  for (int k = 0; k < 2 * NL - 1; k++) {
-    int64_t t = 0;
-    const int lo = k < NL ? 0 : k - NL + 1, hi = k < NL ? k : NL - 1;
-#pragma unroll
-    for (int i = lo; i <= hi; i++) t += (int64_t)A[i] * B[k - i];
-    const int32_t pl = dpp<0x4E>((int32_t)t), ph = dpp<0x4E>((int32_t)(t >> 32));
-    int64_t col = t + (int64_t)(((uint64_t)(uint32_t)ph << 32) | (uint32_t)pl) + carry;
-    if (k < NL) {
-      const int32_t m = mont_digit(col);
-      col += (int64_t)m * (int32_t)P_L[0];
-      if (rr) A[k] = m;
-    } else {
-      r.l[k - NL] = (int32_t)col & MASK28;
-    }
-    carry = col >> 28;
-  }
-  r.l[NL - 1] = (int32_t)carry;
-  return r;
-}
-// own component of a^2 (h_sqr's split) with the product on two lanes (fp_mul_split)
-HP_D Fp h_sqr_split(const Fp& a, bool rr) {
-  const bool ev = lp_even();
-  const Fp pa = dpp_fp<DPP_SWAP>(a);
-  Fp x, y;
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    x.l[i] = pa.l[i] + (ev ? a.l[i] : pa.l[i]);
-    y.l[i] = a.l[i] - (ev ? pa.l[i] : 0);
-  }
-  return fp_mul_split(x, y, rr);
-}
-
 // position of the value a holder lane keeps: role 0 holds (f0, f3), role 1 (f1, f4), role 2 (f2, f5)
 HP_D int cyc_pos(int role, int j) { return role + 3 * j; }
 
 // w0 = six source slots (a byte each, w-basis order); w1 = six destination slots | count << 48 |
 // conjugate-the-result << 56
 HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
-  // lane = 16 row + 4 j + 2 rr + h: squaring j of the row, product half rr (fp_mul_split), component h
+  // lane = 16 row + 4 j + 2 rr + h: squaring j of the row, component h (rr: idle copy)
   const int h = lane & 1, rr = (lane >> 1) & 1, row = lane >> 4, j = (lane >> 2) & 3;
   const bool holder = row < 3 && j < 2;
   const int count = (int)((w1 >> 48) & 0xFF);
@@ -316,12 +268,7 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
   for (int it = 0; it < count; it++) {
     const Fp A = shfl_fp(v, base), B = shfl_fp(v, base + 4);
     const Fp x = j == 2 ? fp_add(A, B) : v;
-#ifndef WV_CYC_SPLIT
-// 1: each product on two lanes (fp_mul_split); measured slower on one box, 3 pairs: combine latency
-// 2.09 vs 2.03 ms, side-stream time 1.90 vs 1.84 ms (profiles/r03/ab_cyc_split.txt)
-#define WV_CYC_SPLIT 0
-#endif
-    const Fp sq = WV_CYC_SPLIT ? h_sqr_split(x, rr != 0) : h_sqr(x);
+    const Fp sq = h_sqr(x);
     const Fp sA = shfl_fp(sq, base), sB = shfl_fp(sq, base + 4), sAB = shfl_fp(sq, base + 8);
     const Fp L = shfl_fp(v, partner);
     // role 0 / 1: pair 0 -> X (r0 / r2), pair 1 -> Y (r3 / r5); role 2: pair 0 -> Z (r1), pair 1 -> X (r4)
@@ -393,11 +340,7 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
     if (special == 2) {
       cyc_run(sm, 2 * pair + h, cur.p0, cur.p1);
     } else if (special == 1) {
-#ifdef WV_SKIP_INV  // timing experiment only: wrong verdicts
-      if (false) {
-#else
       if (pair == 0) {
-#endif
         const Fp v = ld_own(sm, hd.w & 0xFF, h);
         st_own(sm, (hd.w >> 8) & 0xFF, h, fp_reduce(h_inv_vartime(v)));
       }

@@ -64,135 +64,13 @@ HS_MULFN Fp h_mul_l(HS_P14(x), HS_P14(y)) {
   int32_t m[NL];
   int64_t acc = 0;
   Fp r;
-  // HS_NCH > 1: the Z W terms and the reduction terms run in a second chain (sfp.hpp)
 #pragma unroll
   for (int k = 0; k < NL; k++) {
-    int64_t c2 = 0;
 #pragma unroll
     for (int i = 0; i <= k; i++) {
       acc += (int64_t)a.l[i] * Y[k - i];
-      if (HS_NCH > 1) {
-        c2 += (int64_t)Z[i] * W[k - i];
-        HS_CHAIN(c2);
-      } else {
-        acc += (int64_t)Z[i] * W[k - i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < k; i++) {
-      if (HS_NCH > 1) {
-        c2 += (int64_t)m[i] * (int32_t)P_L[k - i];
-        HS_CHAIN(c2);
-      } else {
-        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-      }
-    }
-    if (HS_NCH > 1) acc += c2;
-    m[k] = mont_digit(acc);
-    acc += (int64_t)m[k] * (int32_t)P_L[0];
-    acc >>= 28;
-  }
-#pragma unroll
-  for (int k = NL; k < 2 * NL - 1; k++) {
-    int64_t c2 = 0;
-#pragma unroll
-    for (int i = k - NL + 1; i < NL; i++) {
-      acc += (int64_t)a.l[i] * Y[k - i];
-      if (HS_NCH > 1) {
-        c2 += (int64_t)Z[i] * W[k - i];
-        HS_CHAIN(c2);
-        c2 += (int64_t)m[i] * (int32_t)P_L[k - i];
-        HS_CHAIN(c2);
-      } else {
-        acc += (int64_t)Z[i] * W[k - i];
-        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-      }
-    }
-    if (HS_NCH > 1) acc += c2;
-    r.l[k - NL] = (int32_t)acc & MASK28;
-    acc >>= 28;
-  }
-  r.l[NL - 1] = (int32_t)acc;
-  return r;
-}
-
-HP_D Fp h_mul(const Fp& a, const Fp& b) { return h_mul_l(HS_E14(a), HS_E14(b)); }
-
-// ---------------------------------------------------------------- lazy reduction (HP_LAZY)
-// A sum of products reduced once (Aranha et al., "Faster explicit formulas for computing pairings
-// over ordinary curves", lazy reduction): the products are kept double width -- Fw, 28 limbs of
-// radix 2^28, limbs 0..26 in [0, 2^28) as product scanning leaves them, limb 27 signed -- combined
-// limb-wise (|limb| < 2^31 in every combination below) and Montgomery-reduced by w_red.  An Fp6
-// Karatsuba product then costs 6 x 392 + 3 x 196 MADs per lane instead of 6 x 588.
-// Value contract: |sum| < 2^9 p^2 (Fp6 Karatsuba on inputs < 4p: < 416 p^2), so w_red's output
-// (sum + m p) / 2^392 is normalised and < 1.25 p (p < 2^-11 R), h_mul's output contract.
-#ifndef HP_LAZY
-#define HP_LAZY 0  // bit 0: Fp6 Karatsuba products, bit 1: cyclotomic squarings (both measured slower)
-#endif
-struct Fw {
-  int32_t l[2 * NL];
-};
-// clang's AMDGPU ABI returns an aggregate of more than 16 dwords through memory (a scratch store per
-// dword pair at every call); a 28-element vector comes back in v0..v27
-typedef int32_t FwV __attribute__((ext_vector_type(2 * NL)));
-#define HS_P28(p) HS_P14(p##a), HS_P14(p##b)
-#define HS_E28(x)                                                                                         \
-  x.l[0], x.l[1], x.l[2], x.l[3], x.l[4], x.l[5], x.l[6], x.l[7], x.l[8], x.l[9], x.l[10], x.l[11], x.l[12], \
-      x.l[13], x.l[14], x.l[15], x.l[16], x.l[17], x.l[18], x.l[19], x.l[20], x.l[21], x.l[22], x.l[23],      \
-      x.l[24], x.l[25], x.l[26], x.l[27]
-
-// own component of a * b (Fp2) before reduction: 392 MADs (h_mul_l's operand contract)
-HS_MULFN FwV h_mulw_l(HS_P14(x), HS_P14(y)) {
-  const Fp a = {{HS_L14(x)}};
-  const Fp b = {{HS_L14(y)}};
-  const int32_t sm = lp_even() ? -1 : 0;
-  int32_t Y[NL], W[NL], Z[NL];
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    Y[i] = dpp<DPP_EVEN>(b.l[i]);
-    W[i] = dpp<DPP_ODD>(b.l[i]);
-    Z[i] = (dpp<DPP_SWAP>(a.l[i]) ^ sm) - sm;
-  }
-  int64_t acc = 0;
-  FwV r;
-#pragma unroll
-  for (int k = 0; k < 2 * NL - 1; k++) {
-#pragma unroll
-    for (int i = (k < NL ? 0 : k - NL + 1); i <= (k < NL ? k : NL - 1); i++) {
-      acc += (int64_t)a.l[i] * Y[k - i];
       acc += (int64_t)Z[i] * W[k - i];
     }
-    r[k] = (int32_t)acc & MASK28;
-    acc >>= 28;
-  }
-  r[2 * NL - 1] = (int32_t)acc;
-  return r;
-}
-// x * y in Fp before reduction: 196 MADs (|limb| <= 2^29 for both operands)
-HS_MULFN FwV fp_mulw_l(HS_P14(x), HS_P14(y)) {
-  const Fp a = {{HS_L14(x)}};
-  const Fp b = {{HS_L14(y)}};
-  int64_t acc = 0;
-  FwV r;
-#pragma unroll
-  for (int k = 0; k < 2 * NL - 1; k++) {
-#pragma unroll
-    for (int i = (k < NL ? 0 : k - NL + 1); i <= (k < NL ? k : NL - 1); i++) acc += (int64_t)a.l[i] * b.l[k - i];
-    r[k] = (int32_t)acc & MASK28;
-    acc >>= 28;
-  }
-  r[2 * NL - 1] = (int32_t)acc;
-  return r;
-}
-// Montgomery reduction t / 2^392 of a double-width value with |limb| < 2^31: 196 MADs
-HS_MULFN Fp w_red_l(HS_P28(t)) {
-  const int32_t T[2 * NL] = {HS_L14(ta), HS_L14(tb)};
-  int32_t m[NL];
-  int64_t acc = 0;
-  Fp r;
-#pragma unroll
-  for (int k = 0; k < NL; k++) {
-    acc += T[k];
 #pragma unroll
     for (int i = 0; i < k; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
     m[k] = mont_digit(acc);
@@ -201,62 +79,20 @@ HS_MULFN Fp w_red_l(HS_P28(t)) {
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
-    acc += T[k];
 #pragma unroll
-    for (int i = k - NL + 1; i < NL; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+    for (int i = k - NL + 1; i < NL; i++) {
+      acc += (int64_t)a.l[i] * Y[k - i];
+      acc += (int64_t)Z[i] * W[k - i];
+      acc += (int64_t)m[i] * (int32_t)P_L[k - i];
+    }
     r.l[k - NL] = (int32_t)acc & MASK28;
     acc >>= 28;
   }
-  r.l[NL - 1] = (int32_t)(acc + T[2 * NL - 1]);
+  r.l[NL - 1] = (int32_t)acc;
   return r;
 }
-HP_D Fw fw_of(const FwV& v) {
-  Fw r;
-#pragma unroll
-  for (int i = 0; i < 2 * NL; i++) r.l[i] = v[i];
-  return r;
-}
-HP_D Fw h_mulw(const Fp& a, const Fp& b) { return fw_of(h_mulw_l(HS_E14(a), HS_E14(b))); }
-HP_D Fp w_red(const Fw& t) { return w_red_l(HS_E28(t)); }
-// own component of a^2 before reduction (h_sqr's split, one 196-MAD product)
-HP_D Fw h_sqrw(const Fp& a) {
-  const bool ev = lp_even();
-  Fp x, y;
-#pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const int32_t pa = dpp<DPP_SWAP>(a.l[i]);
-    x.l[i] = pa + (ev ? a.l[i] : pa);
-    y.l[i] = a.l[i] - (ev ? pa : 0);
-  }
-  return fw_of(fp_mulw_l(HS_E14(x), HS_E14(y)));
-}
-// limb-wise combinations (no carries)
-HP_D Fw w_add(const Fw& a, const Fw& b) {
-  Fw r;
-#pragma unroll
-  for (int i = 0; i < 2 * NL; i++) r.l[i] = a.l[i] + b.l[i];
-  return r;
-}
-HP_D Fw w_sub(const Fw& a, const Fw& b) {
-  Fw r;
-#pragma unroll
-  for (int i = 0; i < 2 * NL; i++) r.l[i] = a.l[i] - b.l[i];
-  return r;
-}
-HP_D Fw w_sub2(const Fw& a, const Fw& b, const Fw& c) {
-  Fw r;
-#pragma unroll
-  for (int i = 0; i < 2 * NL; i++) r.l[i] = a.l[i] - b.l[i] - c.l[i];
-  return r;
-}
-// own component of xi t (xi = 1 + u): even t0 - t1, odd t1 + t0
-HP_D Fw w_xi(const Fw& t) {
-  const int32_t sm = lp_even() ? -1 : 0;
-  Fw r;
-#pragma unroll
-  for (int i = 0; i < 2 * NL; i++) r.l[i] = t.l[i] + ((dpp<DPP_SWAP>(t.l[i]) ^ sm) - sm);
-  return r;
-}
+
+HP_D Fp h_mul(const Fp& a, const Fp& b) { return h_mul_l(HS_E14(a), HS_E14(b)); }
 
 // own component of a^2: even (a0 + a1)(a0 - a1), odd (a1 + a1) a0... written as x * y with
 // x = pa + (even ? a : pa), y = a - (even ? pa : 0)  (odd lane: x = 2 a0, y = a1)
@@ -380,17 +216,6 @@ HP_D H6 h6_mul_v(const H6& a) { return {h_mul_xi(a.c2), a.c0, a.c1}; }
 
 // Karatsuba, inputs < 4p
 HP_D H6 h6_mul(const H6& a, const H6& b) {
-#if HP_LAZY & 1
-  // c0 = v0 + xi (t0 - v1 - v2), c1 = t1 - v0 - v1 + xi v2, c2 = t2 - v0 - v2 + v1: three reductions
-  const Fw v1 = h_mulw(a.c1, b.c1);
-  const Fw v2 = h_mulw(a.c2, b.c2);
-  const Fw d0 = w_sub2(h_mulw(fp_addl(a.c1, a.c2), fp_add(b.c1, b.c2)), v1, v2);
-  const Fw v0 = h_mulw(a.c0, b.c0);
-  const Fp c0 = w_red(w_add(v0, w_xi(d0)));
-  const Fp c2 = w_red(w_add(w_sub2(h_mulw(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2)), v0, v2), v1));
-  const Fp c1 = w_red(w_add(w_sub2(h_mulw(fp_addl(a.c0, a.c1), fp_add(b.c0, b.c1)), v0, v1), w_xi(v2)));
-  return {c0, c1, c2};
-#else
   const Fp v0 = h_mul(a.c0, b.c0);
   const Fp v1 = h_mul(a.c1, b.c1);
   const Fp v2 = h_mul(a.c2, b.c2);
@@ -399,7 +224,6 @@ HP_D H6 h6_mul(const H6& a, const H6& b) {
   const Fp t2 = h_mul(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2));
   return {fp_add(v0, h_mul_xi(fp_sub(fp_subl(t0, v1), v2))), fp_add(fp_sub(fp_subl(t1, v0), v1), h_mul_xi(v2)),
           fp_add(fp_sub(fp_subl(t2, v0), v2), v1)};
-#endif
 }
 // x (a + b v)
 HP_D H6 h6_mul_01(const H6& x, const Fp& a, const Fp& b) {
@@ -524,25 +348,6 @@ HP_D H12 h12_cyclo_sqr(const H12& f) {
   const Fp& a0 = f.c0.c0; const Fp& a2 = f.c0.c1; const Fp& a4 = f.c0.c2;
   const Fp& a1 = f.c1.c0; const Fp& a3 = f.c1.c1; const Fp& a5 = f.c1.c2;
   H12 r;
-#if HP_LAZY & 2
-  // 9 unreduced squares, 6 reductions (one per output) instead of 9
-  {
-    const Fw s0 = h_sqrw(a0), s3 = h_sqrw(a3);
-    r.c0.c0 = fp_red_mk<3, -2>(w_red(w_add(s0, w_xi(s3))), a0);
-    r.c1.c1 = fp_red_mk<3, 2>(w_red(w_sub2(h_sqrw(fp_add(a0, a3)), s0, s3)), a3);
-  }
-  {
-    const Fw s1 = h_sqrw(a1), s4 = h_sqrw(a4);
-    r.c0.c1 = fp_red_mk<3, -2>(w_red(w_add(s1, w_xi(s4))), a2);
-    r.c1.c2 = fp_red_mk<3, 2>(w_red(w_sub2(h_sqrw(fp_add(a1, a4)), s1, s4)), a5);
-  }
-  {
-    const Fw s2 = h_sqrw(a2), s5 = h_sqrw(a5);
-    r.c0.c2 = fp_red_mk<3, -2>(w_red(w_add(s2, w_xi(s5))), a4);
-    r.c1.c0 = fp_red_mk<3, 2>(w_red(w_xi(w_sub2(h_sqrw(fp_add(a2, a5)), s2, s5))), a1);
-  }
-  return r;
-#endif
   {
     const Fp s0 = h_sqr(a0), s3 = h_sqr(a3), s03 = h_sqr(fp_add(a0, a3));
     r.c0.c0 = fp_red_mk<3, -2>(h_add_xi_l(s0, s3), a0);

@@ -31,26 +31,6 @@
 #define HS_MULFN HS_HD
 #endif
 
-// HS_NCH = 2: each product column is accumulated in two independent int64 chains (products of
-// the operands in one, the Montgomery reduction terms in the other), merged once per column.
-// LLVM folds every `acc += x * y` into one v_mad_i64_i32 chain, and a dependent MAD waits for its
-// predecessor; two chains let the MAD pipe overlap them (tools/ubench_v2: 25.0 -> 29.1 T MAD/s for
-// one vs two chains at two waves per SIMD).  The empty asm keeps LLVM from re-associating the
-// second chain back into the first.
-#ifndef HS_NCH
-#define HS_NCH 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-#define HS_CHAIN(x) \
-  do {              \
-    if (HS_NCH > 1) asm("" : "+v"(x)); \
-  } while (0)
-#else
-#define HS_CHAIN(x) \
-  do {              \
-  } while (0)
-#endif
-
 namespace hbs {
 
 using hb::NL;
@@ -106,37 +86,21 @@ HS_MULFN Fp fp_mul_l(HS_P14(x), HS_P14(y)) {
   Fp r;
 #pragma unroll
   for (int k = 0; k < NL; k++) {
-    int64_t red = 0;  // second chain (HS_NCH > 1): reduction terms of this column
 #pragma unroll
     for (int i = 0; i <= k; i++) acc += (int64_t)a.l[i] * b.l[k - i];
 #pragma unroll
-    for (int i = 0; i < k; i++) {
-      if (HS_NCH > 1) {
-        red += (int64_t)m[i] * (int32_t)P_L[k - i];
-        HS_CHAIN(red);
-      } else {
-        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-      }
-    }
-    if (HS_NCH > 1) acc += red;
+    for (int i = 0; i < k; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
     m[k] = mont_digit(acc);
     acc += (int64_t)m[k] * (int32_t)P_L[0];
     acc >>= 28;
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
-    int64_t red = 0;
 #pragma unroll
     for (int i = k - NL + 1; i < NL; i++) {
       acc += (int64_t)a.l[i] * b.l[k - i];
-      if (HS_NCH > 1) {
-        red += (int64_t)m[i] * (int32_t)P_L[k - i];
-        HS_CHAIN(red);
-      } else {
-        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-      }
+      acc += (int64_t)m[i] * (int32_t)P_L[k - i];
     }
-    if (HS_NCH > 1) acc += red;
     r.l[k - NL] = (int32_t)acc & MASK28;
     acc >>= 28;
   }
@@ -156,17 +120,8 @@ HS_MULFN Fp fp_sqr_l(HS_P14(x)) {
     for (int i = 0; i < (k + 1) / 2; i++) cr += (int64_t)a.l[i] * a.l[k - i];
     acc += cr * 2;
     if ((k & 1) == 0) acc += (int64_t)a.l[k / 2] * a.l[k / 2];
-    int64_t red = 0;
 #pragma unroll
-    for (int i = 0; i < k; i++) {
-      if (HS_NCH > 1) {
-        red += (int64_t)m[i] * (int32_t)P_L[k - i];
-        HS_CHAIN(red);
-      } else {
-        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-      }
-    }
-    if (HS_NCH > 1) acc += red;
+    for (int i = 0; i < k; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
     m[k] = mont_digit(acc);
     acc += (int64_t)m[k] * (int32_t)P_L[0];
     acc >>= 28;
@@ -178,17 +133,8 @@ HS_MULFN Fp fp_sqr_l(HS_P14(x)) {
     for (int i = k - NL + 1; i < (k + 1) / 2; i++) cr += (int64_t)a.l[i] * a.l[k - i];
     acc += cr * 2;
     if ((k & 1) == 0) acc += (int64_t)a.l[k / 2] * a.l[k / 2];
-    int64_t red = 0;
 #pragma unroll
-    for (int i = k - NL + 1; i < NL; i++) {
-      if (HS_NCH > 1) {
-        red += (int64_t)m[i] * (int32_t)P_L[k - i];
-        HS_CHAIN(red);
-      } else {
-        acc += (int64_t)m[i] * (int32_t)P_L[k - i];
-      }
-    }
-    if (HS_NCH > 1) acc += red;
+    for (int i = k - NL + 1; i < NL; i++) acc += (int64_t)m[i] * (int32_t)P_L[k - i];
     r.l[k - NL] = (int32_t)acc & MASK28;
     acc >>= 28;
   }

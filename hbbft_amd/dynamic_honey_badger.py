@@ -121,23 +121,31 @@ class DhbKeyGen:
         batch's contribution order.  Returns the Step: faults (InvalidKeyGenMessageEra /
         InvalidKeyGenMessageSignature against the PROPOSER, SyncKeyGenPart(..) / SyncKeyGenAck(..)
         / UnexpectedKeyGen* against the signer) and the signed Acks our valid Parts produce."""
-        flat = [(pid, skm) for pid, msgs in contributions for skm in msgs]
-        for pid, msgs in contributions:  # key_gen_msg_buffer.retain(|skgm| !committed.contains(skgm))
-            committed = {(m.era, m.node_id, key_gen_msg_bytes(m.msg), m.sig) for m in msgs}
-            self.key_gen_msg_buffer = [m for m in self.key_gen_msg_buffer
-                                       if (m.era, m.node_id, key_gen_msg_bytes(m.msg), m.sig) not in committed]
-        in_era = [(pid, skm) for pid, skm in flat if skm.era == self.era]
-        sig_ok = dict(zip((id(s) for _, s in in_era),
-                          self.verify_signatures([(s.node_id, s.sig, s.msg) for _, s in in_era])))
+        # The reference (:333-347) runs, per contribution in batch order, key_gen_msg_buffer.retain(|m|
+        # !committed_i.contains(m)) and then handles that contribution's messages -- which may buffer new
+        # signed Acks (send_transaction).  Messages already buffered are removed by every retain either
+        # way, so the retains are applied to them up front; a message buffered while handling
+        # contribution i is filtered by the retains of the contributions AFTER i only (``later[i]``).
+        # The signature checks and SyncKeyGen calls stay batched across contributions.
+        flat = [(ci, pid, skm) for ci, (pid, msgs) in enumerate(contributions) for skm in msgs]
+        keyed = [{_skm_key(m) for m in msgs} for _, msgs in contributions]
+        later = [set() for _ in contributions]
+        acc = set()
+        for ci in range(len(contributions) - 1, -1, -1):
+            later[ci] = acc
+            acc = acc | keyed[ci]
+        self.key_gen_msg_buffer = [m for m in self.key_gen_msg_buffer if _skm_key(m) not in acc]
+        in_era = [skm for _, _, skm in flat if skm.era == self.era]
+        sig_ok = dict(zip((id(s) for s in in_era), self.verify_signatures([(s.node_id, s.sig, s.msg) for s in in_era])))
         step = Step()
-        run = []  # consecutive verified messages of one kind, handled in one SyncKeyGen call
+        run = []  # consecutive verified messages of one kind, handled in one SyncKeyGen call: (ci, skm)
 
         def flush():
             if run:
-                step.extend(self._handle_run(run, rng))
+                step.extend(self._handle_run(run, rng, later))
                 run.clear()
 
-        for pid, skm in flat:
+        for ci, pid, skm in flat:
             if skm.era != self.era:
                 flush()
                 step.fault_log.append(Fault(pid, "InvalidKeyGenMessageEra"))
@@ -145,32 +153,42 @@ class DhbKeyGen:
                 flush()
                 step.fault_log.append(Fault(pid, "InvalidKeyGenMessageSignature"))
             else:
-                if run and type(run[0].msg) is not type(skm.msg):
+                if run and type(run[0][1].msg) is not type(skm.msg):
                     flush()
-                run.append(skm)
+                run.append((ci, skm))
         flush()
         return step
 
-    def _handle_run(self, run, rng):
+    def _handle_run(self, run, rng, later):
         if self.key_gen is None:  # no key generation ongoing (:444-447, :465-468)
-            kind = "UnexpectedKeyGenPart" if isinstance(run[0].msg, Part) else "UnexpectedKeyGenAck"
-            return Step(fault_log=[Fault(m.node_id, kind) for m in run])
+            kind = "UnexpectedKeyGenPart" if isinstance(run[0][1].msg, Part) else "UnexpectedKeyGenAck"
+            return Step(fault_log=[Fault(m.node_id, kind) for _, m in run])
         step = Step()
-        if isinstance(run[0].msg, Part):
-            outs = self.key_gen.handle_parts([(m.node_id, m.msg) for m in run], rng)
-            acks = []
-            for m, o in zip(run, outs):
+        if isinstance(run[0][1].msg, Part):
+            outs = self.key_gen.handle_parts([(m.node_id, m.msg) for _, m in run], rng)
+            acks, acis = [], []
+            for (ci, m), o in zip(run, outs):
                 if o.fault is not None:
                     step.fault_log.append(Fault(m.node_id, "SyncKeyGenPart(%s)" % o.fault))
                 elif o.ack is not None:
                     acks.append(o.ack)
+                    acis.append(ci)
+            first = len(self.key_gen_msg_buffer)
             step.extend(self.send_transactions(acks))
+            if self.is_validator and acks:  # the later contributions' retains on the Acks just buffered
+                fresh = self.key_gen_msg_buffer[first:]
+                self.key_gen_msg_buffer[first:] = [m for m, ci in zip(fresh, acis) if _skm_key(m) not in later[ci]]
         else:
-            outs = self.key_gen.handle_acks([(m.node_id, m.msg) for m in run])
-            for m, o in zip(run, outs):
+            outs = self.key_gen.handle_acks([(m.node_id, m.msg) for _, m in run])
+            for (_, m), o in zip(run, outs):
                 if o.fault is not None:
                     step.fault_log.append(Fault(m.node_id, "SyncKeyGenAck(%s)" % o.fault))
         return step
+
+
+def _skm_key(m):
+    """Equality of SignedKeyGenMsg (era, node_id, message, signature), as the reference's retain uses."""
+    return (m.era, m.node_id, key_gen_msg_bytes(m.msg), bytes(m.sig))
 
 
 # ================================================================ votes (src/dynamic_honey_badger/votes.rs)

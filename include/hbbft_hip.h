@@ -170,8 +170,9 @@ int hbh_interpolate_g1(hbh_engine* eng, size_t ncomb, int t, const uint32_t* idx
  * verdict[c] = PublicKey::verify_g2(out[c], hashes[c]) = (e(master_pk, H_c) == e(g1, out[c]))
  * (:260-266) without a host round trip in between.  status[c] as hbh_interpolate_g2; verdict[c]
  * = 0 is the reference's Error::VerificationFailed; verdicts of a combine whose status is not
- * HBH_OK are meaningless (the reference returns the combine error first).  Calls of at most 1,280
- * one-pair Miller waves (ncomb x (t + 2); at most 384 combines) evaluate the same verdict as prod_k e(lambda_k g1, share_k) * e(-master_pk, H_c) == 1 on a
+ * HBH_OK are meaningless (the reference returns the combine error first).  A master_pk coordinate
+ * >= p is HBH_ERR_ARG.  Calls of at most 540 + 24 t one-pair Miller waves (ncomb x (t + 2); at most
+ * 384 combines) evaluate the same verdict as prod_k e(lambda_k g1, share_k) * e(-master_pk, H_c) == 1 on a
  * second stream while the first interpolates ("split master check"; the environment
  * variable HBH_SPLIT_CHECK=0 at engine creation selects interpolate-then-verify for every size;
  * HBH_SPLIT_MAX=<n> replaces the wave-count rule by "at most n combines per call"). */
@@ -211,7 +212,9 @@ int hbh_bivar_ack_check(hbh_engine* eng, size_t nack, int t, size_t nparts, cons
  * in HBM, uploaded once, plus the Jacobian rows row(x) computed so far; calls name parts by their
  * index in the set and upload only indices and values.
  *   hbh_commit_set_create / _destroy: an empty set of degree t on `eng` (destroy waits for the
- *     engine's work).
+ *     engine's work).  The engine owns its sets' device memory: hbh_engine_destroy frees it and
+ *     detaches the sets, after which every call on such a set returns HBH_ERR_ARG and
+ *     hbh_commit_set_destroy only frees the handle (either destruction order is safe).
  *   hbh_commit_set_add: append nparts commitments ((t+1)(t+2)/2 ABI G1 points each, coeff_pos
  *     order); *first (may be NULL) = the set index of the first one.
  *   hbh_commit_set_size: commitments and cached rows held.

@@ -91,3 +91,34 @@ def test_config3_network_acks(engine):
         rhs = cbls.g1_mul(G1, int.from_bytes(bytes(vals[a]), "little"))
         assert (lhs == rhs) == bool(got[a]), a
     cs.close()
+
+
+def test_commit_set_outlives_engine():
+    """a set closed after its engine must not touch the freed engine.  hbh_engine_destroy
+    frees the set's device memory and detaches it; later calls on the set fail loudly, and closing it
+    (explicitly or from __del__) is safe."""
+    from hbbft_amd.engine import Engine
+
+    eng = Engine(0)
+    rng = random.Random(62)
+    t = 2
+    npos = (t + 1) * (t + 2) // 2
+    coefs = [rng.randrange(R) for _ in range(npos)]
+    cs = eng.commit_set(t)
+    cs.add([eng.g1_mul_gen(coefs)])
+    assert cs.size() == (1, 0)
+    before = cs.ack_check([0], [1], [2], [f_eval(coefs, t, 1, 2)])
+    assert before == b"\x01"
+    eng.close()
+    with pytest.raises(HbhError):
+        cs.ack_check([0], [1], [2], [f_eval(coefs, t, 1, 2)])
+    with pytest.raises(HbhError):
+        cs.add([[G1] * npos])
+    cs.close()
+    cs.close()
+    # and the other order on a fresh engine: set first, then engine
+    eng2 = Engine(0)
+    cs2 = eng2.commit_set(t)
+    cs2.add([eng2.g1_mul_gen(coefs)])
+    cs2.close()
+    eng2.close()

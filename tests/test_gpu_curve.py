@@ -7,6 +7,8 @@ import random
 
 import pytest
 
+from hbbft_amd._lib import HbhError
+
 from oracle import bls12_381 as C
 from oracle import cbls, tc
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
@@ -153,7 +155,7 @@ def unsplit_engine():
 
 @pytest.mark.parametrize("t", [0, 1, 21, 70])
 def test_combine_verify_split_matches_unsplit(engine, unsplit_engine, t):
-    """Calls of at most 1,280 one-pair Miller waves (ncomb x (t + 2)) take the split master check
+    """Calls of at most 540 + 24 t one-pair Miller waves (ncomb x (t + 2)) take the split master check
     (partial Miller loops of (lambda_k g1, sigma_k) and (-mpk, H) beside the interpolation, one final
     exponentiation per combine); larger calls, and an engine created with HBH_SPLIT_CHECK=0, the
     interpolate-then-verify form.  Same signatures, statuses and verdicts on the same inputs:
@@ -191,6 +193,17 @@ def test_combine_verify_split_matches_unsplit(engine, unsplit_engine, t):
     assert [cbls.verify_g2(mpk, s, h) for s, h in zip(out9[:5], hashes[:5])] == [bool(x) for x in v9[:5]]
     if t > 0:
         assert st9[5] == 5 and v9[5] == 0
+    # master key at infinity (the split form's Z = 0 inactive pair): identical on both forms; the
+    # signature then verifies only if it is the point at infinity too
+    inf = bytes(96)
+    assert engine.combine_verify_g2(t, idx, pts, inf, hashes) == unsplit_engine.combine_verify_g2(t, idx, pts, inf,
+                                                                                                  hashes)
+    # a master key coordinate >= p is an argument error on both forms
+    bad = bytearray(mpk)
+    bad[0:48] = (C.P + 1).to_bytes(48, "little")
+    for eng in (engine, unsplit_engine):
+        with pytest.raises(HbhError):
+            eng.combine_verify_g2(t, idx[:1], pts[:1], bytes(bad), hashes[:1])
 
 
 def test_interpolate_edge_cases(engine):

@@ -58,3 +58,38 @@ def test_dhb_key_gen_signed_messages(engine):
     idle = DhbKeyGen(engine, era, 0, sks[0], pub)
     step = idle.handle_committed([(0, [contributions[0][1][0]])])
     assert [(f.node_id, f.kind) for f in step.fault_log] == [(0, "UnexpectedKeyGenAck")]
+
+
+def test_dhb_retain_runs_per_contribution(engine):
+    """key_gen_msg_buffer.retain runs per contribution in batch order, BEFORE that contribution's
+    messages are handled (src/dynamic_honey_badger/dynamic_honey_badger.rs:333-347): a signed Ack our
+    node buffers while handling contribution i is removed by the retain of a LATER contribution that
+    commits the same message, and survives one committed EARLIER.  Two replicas of node 0
+    with identical seeds produce identical Acks; the second sees its own future Acks committed."""
+    rng = random.Random(78)
+    n, t, era = 4, 1, 3
+    sks = [rng.randrange(1, R_ORDER) for _ in range(n)]
+    pub = dict(enumerate(hoststage.g1_mul([G1_GEN] * n, sks)))
+    parts = [SyncKeyGen.new(i, sks[i], pub, t, engine, rng=rng)[1] for i in range(1, n)]
+
+    def replica():
+        kg, part0 = SyncKeyGen.new(0, sks[0], pub, t, engine, rng=random.Random(5))
+        return DhbKeyGen(engine, era, 0, sks[0], pub, key_gen=kg), part0
+
+    def signed(i, msg):
+        return SignedKeyGenMsg(era, i, msg, hoststage.g2_mul(hoststage.hash_g2([key_gen_msg_bytes(msg)]), [sks[i]])[0])
+
+    a, part0 = replica()
+    allparts = [part0] + parts
+    contributions = [(i, [signed(i, allparts[i])]) for i in range(n)]
+    a.handle_committed(contributions, random.Random(6))
+    acks = list(a.key_gen_msg_buffer)
+    assert len(acks) == n and all(m.node_id == 0 for m in acks)
+    b, _ = replica()
+    later = [(i, list(m)) for i, m in contributions]
+    later[3][1].append(acks[1])      # the Ack for contribution 1's Part, committed by contribution 3
+    later[0][1].append(acks[2])      # the Ack for contribution 2's Part, committed BEFORE it exists
+    b.handle_committed(later, random.Random(6))
+    keys = [(m.node_id, key_gen_msg_bytes(m.msg), bytes(m.sig)) for m in b.key_gen_msg_buffer]
+    want = [(m.node_id, key_gen_msg_bytes(m.msg), bytes(m.sig)) for m in (acks[0], acks[2], acks[3])]
+    assert keys == want
