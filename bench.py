@@ -17,6 +17,7 @@ construction.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
 import random
@@ -44,9 +45,14 @@ MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
 IMPLS = {"auto": 3, "pair": 4, "wave": 5}   # HBH_IMPL_* (include/hbbft_hip.h)
-KERNEL_NAMES = {"pair": "hbs::k_pair_verify<false, true, 2>",
+# the lane-pair check runs as three kernels (csrc/k_pair.hip: lines, f, final exponentiation); its
+# roofline entry is the whole pairing stage, and its traffic the three kernels' sum
+PAIR_SIGN = ("hbs::k_pair_lines<false, true, 2>", "hbs::k_pair_f", "hbs::k_pair_fe")
+PAIR_DECRYPT = ("hbs::k_pair_lines<false, false, 0>", "hbs::k_pair_f", "hbs::k_pair_fe")
+KERNEL_NAMES = {"pair": " + ".join(PAIR_SIGN),
                 "wave": "hbs::k_wave (one wave per check)",
-                "auto": "hbs::k_pair_verify<false, true, 2>"}
+                "auto": " + ".join(PAIR_SIGN),
+                "decrypt": " + ".join(PAIR_DECRYPT)}
 G1_UNC = bytes.fromhex(
     "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
     "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
@@ -219,7 +225,7 @@ def timed_steps(step, streams, steps, world, dev):
     return (allreduce_max(ms, dev) if world > 1 else ms) / steps
 
 
-def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_simd=None):
+def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_simd=None, source=None):
     """One kernel's roofline: achieved = units per launch x algorithmic MADs per unit (workcount,
     300 per Fp-mul, 222 per Fp-sqr) / average launch time (HIP events on the engine's stream)."""
     from hbbft_amd import workcount
@@ -228,7 +234,8 @@ def roofline_entry(kernel, launches, avg_ms, units, op, unit_name, waves_per_sim
     e = {"kernel": kernel, "launches": launches, "avg_launch_ms": avg_ms, "units_per_launch": units,
          "unit": unit_name, "fp_ops_per_unit": op[0], "fp_sqr_per_unit": op[1], "mad_per_unit": mad,
          "achieved": achieved, "peak": MAD_PEAK_MEASURED, "frac": achieved / MAD_PEAK_MEASURED,
-         "peak_theoretical": MAD_PEAK_THEORETICAL, "traffic": pmc_traffic(kernel)}
+         "peak_theoretical": MAD_PEAK_THEORETICAL}
+    e.update(traffic_fields(kernel, source))
     if waves_per_simd:
         if waves_per_simd < 1:  # below one wave per SIMD on average: the 1-wave ceiling scaled by occupancy
             ceil = MAD_CEILING_BY_WAVES[1] * waves_per_simd
@@ -254,7 +261,7 @@ def reference_work(main_k, workcount):
 
 
 def pair_waves_per_simd(checks):
-    """k_pair_verify: two lanes per check, 64-lane waves, 1,024 SIMDs."""
+    """The lane-pair kernels (k_pair_lines / k_pair_f / k_pair_fe): two lanes per check, 64-lane waves, 1,024 SIMDs."""
     w = checks * 2 / 64 / 1024
     return 2 if w >= 2 else (1 if w >= 1 else round(w, 3))
 
@@ -323,17 +330,36 @@ def cpu_baseline(w, budget_s=12.0):
                           "cgroup quota, OMP_NUM_THREADS); nproc %d counts the whole machine" % (threads, ncpu)}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the latest committed rocprofv3 --pmc passes
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/<round>/pmc_traffic.json), or None
-    when no committed profile covers that kernel."""
+def traffic_fields(kernel, source=None):
+    """roofline "traffic" (HBM bytes per launch, or None) and "traffic_source" (profile file, its
+    commit, whether it measured the library loaded now).  kernel: a name, or names joined by " + "
+    (summed); source: the bench workload whose profile to prefer (kernels shared between workloads)."""
+    d = pmc_traffic(kernel.split(" + "), source)
+    return {"traffic": d["hbm_bytes_per_launch"] if d else None, "traffic_source": d}
+
+
+def pmc_traffic(kernels, source=None):
+    """HBM bytes per launch of `kernels` (summed) from the latest committed rocprofv3 --pmc passes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/<round>/pmc_traffic.json), with the file
+    it came from and whether those passes ran the library this process loaded (sha256 of the .so the
+    profile recorded vs the loaded one); None when no committed profile covers every kernel."""
     import glob
+    import hashlib
+    from hbbft_amd import _lib
+    try:
+        loaded = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    except OSError:
+        loaded = None
     for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
         with open(fn) as f:
             d = json.load(f)
-        k = d.get("kernels", {}).get(kernel)
-        if k is not None:
-            return k.get("hbm_bytes_per_launch")
+        table = d.get("by_source", {}).get(source) if source else None
+        if not table or not all(k in table for k in kernels):
+            table = d.get("kernels", {})
+        if all(k in table for k in kernels):
+            return {"hbm_bytes_per_launch": sum(table[k].get("hbm_bytes_per_launch") or 0 for k in kernels),
+                    "profile": os.path.relpath(fn, ROOT), "profile_commit": d.get("git_commit"),
+                    "matches_loaded_lib": (d.get("lib_sha256") == loaded) if d.get("lib_sha256") else None}
     return None
 
 
@@ -529,7 +555,7 @@ def main():
                        "parallelism": "shard-by-batch x%d" % world},
             "verdicts_ok": ok, "per_rank": per_rank, "reference_work": reference_work(main_k, workcount),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
-                             traffic=pmc_traffic(KERNEL_NAMES[args.impl]), kernels=kernels,
+                             **traffic_fields(KERNEL_NAMES[args.impl], "sign"), kernels=kernels,
                              note="achieved = checks x algorithmic MADs per check (workcount.PAIR_CHECK_WALK: "
                                   "2-pair Miller + sigma G2 walk + final exp; 300 MAD/Fp-mul, 222/Fp-sqr) / "
                                   "average launch time of isolated single-stream launches (the throughput value alternates two "
@@ -649,11 +675,14 @@ def run_decrypt(args, eng, world, rank, dev):
     eng.set_profiling(False)
     want = eng.g1_mul(us, [coeffs[0]] * len(mine))
     ok = ok and out == want and all(x == 0 for x in st)
-    per_rank = gather_per_rank({"rank": rank, "checks": n, "ciphertexts": len(mine),
+    per_rank = gather_per_rank({"rank": rank, "checks": n, "ciphertexts": len(mine), "first_check": lo,
                                 "kernel_ms": pair_ms / max(pair_n, 1), "ms_per_step": ms_step, "ok": ok}, world)
     ok = all(r["ok"] for r in per_rank)
+    # the gathered outputs (verdicts of the last step, combined G1 points), in rank order = batch order:
+    # their digests equal the one-rank run's when the shards are right (tests/test_bench_launch.py)
+    blobs = gather_per_rank((d_vs[0].cpu().numpy()[:n].tobytes(), b"".join(out)), world)
     if rank == 0:
-        main_k = roofline_entry("hbs::k_pair_verify<false, false, 0>", pair_n, pair_ms / max(pair_n, 1), n,
+        main_k = roofline_entry(KERNEL_NAMES["decrypt"], pair_n, pair_ms / max(pair_n, 1), n,
                                 workcount.PAIR_CHECK_TABLE, "decryption-share check", pair_waves_per_simd(n))
         kernels = [main_k]
         if prep_n:
@@ -668,11 +697,13 @@ def run_decrypt(args, eng, world, rank, dev):
             "config": {"workload": "ThresholdDecrypt, BASELINE configs[2]", "total_checks": total, "streams": len(streams),
                        "ciphertexts": ncts, "parallelism": "shard-by-ciphertext x%d" % world},
             "verdicts_ok": ok, "combines_ok": out == want, "per_rank": per_rank,
+            "verdicts_sha256": hashlib.sha256(b"".join(b[0] for b in blobs)).hexdigest(),
+            "combines_sha256": hashlib.sha256(b"".join(b[1] for b in blobs)).hexdigest(),
             "reference_work": reference_work(main_k, workcount),
             "combines_per_s_rank0": len(mine) / comb_s,                 # host-to-host, one call
             "combines_per_s_rank0_device": len(mine) / (comb_dev_ms / 1e3),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
-                             traffic=pmc_traffic("hbs::k_pair_verify<false, false, 0>"), kernels=kernels,
+                             **traffic_fields(KERNEL_NAMES["decrypt"], "decrypt"), kernels=kernels,
                              note="both G2 sides (H_uv, W) are per-ciphertext line tables: per check = 2-pair "
                                   "Miller + final exp (workcount.PAIR_CHECK_TABLE)"),
         }
@@ -737,7 +768,10 @@ def dkg_workload(eng, seed, n_nodes, t, nodes, tamper_every=97):
     xs = np.repeat(np.array(nodes, dtype=np.uint32), n_nodes * n_nodes)
     ys = np.tile(np.arange(1, n_nodes + 1, dtype=np.uint32), nx * n_nodes)
     flat = [int(vals[p][k][y]) for k in range(nx) for p in range(n_nodes) for y in range(n_nodes)]
-    bad = set(range(0, n, tamper_every))
+    # tampered: every tamper_every-th ack of the WHOLE network's order (x, p, y), so a node's acks
+    # are the same whichever ranks check it (the rank split of tests/test_bench_launch.py)
+    nn = n_nodes * n_nodes
+    bad = {k * nn + a for k, x in enumerate(nodes) for a in range((-(x - 1) * nn) % tamper_every, nn, tamper_every)}
     for a in bad:
         flat[a] = (flat[a] + 1) % R_ORDER
     vb = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in flat), dtype=np.uint8).reshape(n, 32)
@@ -804,12 +838,19 @@ def run_dkg(args, eng, world, rank, dev):
             eng.g1_mul_gen(sc)
             ts_.append((time.perf_counter() - t0) * 1e3)
         commit_ms[k] = statistics.median(ts_)
+    enc = dkg_encrypt_cost(eng, n_nodes, t)
     ms = _max_over_ranks(dev_ms, world, dev)
     host_ms = _max_over_ranks(statistics.median(times), world, dev)
     per_rank = gather_per_rank({"rank": rank, "device_ms": dev_ms, "host_ms": statistics.median(times), "ok": ok,
-                                "acks": nack, "nodes": len(nodes)}, world)
+                                "acks": nack, "nodes": len(nodes), "node_list": nodes}, world)
     ok = all(r["ok"] for r in per_rank)
     total = sum(r["acks"] for r in per_rank)
+    # verdicts per checking node, gathered: the digest over nodes in order equals the one-rank run's
+    xa = np.asarray(xs)
+    vb = np.frombuffer(bytes(v), dtype=np.uint8)
+    by_node = {}
+    for part in gather_per_rank({int(x): vb[xa == x].tobytes() for x in nodes}, world):
+        by_node.update(part)
     if rank == 0:
         ops = [workcount.bivar_ack(t, y) for y in range(1, n_nodes + 1)]
         op = (sum(o[0] for o in ops) / n_nodes, sum(o[1] for o in ops) / n_nodes)
@@ -832,9 +873,11 @@ def run_dkg(args, eng, world, rank, dev):
                                  "resident in HBM (commitment set); host_to_host_ms: the whole call incl. the "
                                  "upload of indices and values"},
             "host_to_host_ms": host_ms, "row_build_ms": row_ms, "rows": len(nodes) * n_nodes,
+            "encrypt": enc,
             "bivar_commitment_ms": {"1 part (595 points)": commit_ms[1], "100 parts (59,500 points)": commit_ms[n_nodes],
                                     "note": "BivarPoly::commitment on the comb table (hbh_g1_mul_gen), host-to-host"},
             "data_gen_s": round(gen_s, 2), "verdicts_ok": ok, "per_rank": per_rank,
+            "verdicts_sha256": hashlib.sha256(b"".join(by_node[x] for x in sorted(by_node))).hexdigest(),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
                              note="%s; %.1f waves per SIMD launched" % (
                                  "one lane per ack on affine rows" if lane else "four lanes per ack (lane quads)",
@@ -845,6 +888,42 @@ def run_dkg(args, eng, world, rank, dev):
             line["cpu_baseline"] = cpu_baseline_dkg(t, commits, pidx, xs, ys, vals, expected, eng)
         print(json.dumps(line), flush=True)
     cs.close()
+
+
+def dkg_encrypt_cost(eng, n_nodes, t, reps=3):
+    """The DKG's generation side: PublicKey::encrypt_with_rng of one Part's N rows
+    (src/sync_key_gen.rs:346-357: bincode Poly of t+1 Fr, 1,096 B) and of one Ack's N values (:386-390:
+    32-byte Fr) on the host stage (hbh_encrypt: U = g1 r, V = msg ^ hash(pk r), W = hash_g1_g2(U, V) r),
+    host-to-host, median of reps.  A node encrypts one Part and one Ack per Part it accepts:
+    N + N^2 encryptions per DKG (10,100 at N = 100)."""
+    from hbbft_amd import hoststage
+    from hbbft_amd.sync_key_gen import ser_row
+    rng = random.Random(11)
+    g1 = g1a_abi()
+    pks = eng.g1_mul([g1] * n_nodes, [rng.randrange(1, R_ORDER) for _ in range(n_nodes)])
+    rows = [ser_row([rng.randrange(R_ORDER) for _ in range(t + 1)]) for _ in range(n_nodes)]
+    vals = [rng.randrange(R_ORDER).to_bytes(32, "little") for _ in range(n_nodes)]
+    threads = hoststage.host_threads()
+    out = {}
+    for name, msgs in (("part_rows_ms", rows), ("ack_values_ms", vals)):
+        ts_ = []
+        for _ in range(reps):
+            nonces = [rng.randrange(1, R_ORDER) for _ in msgs]
+            t0 = time.perf_counter()
+            hoststage.encrypt(pks, msgs, nonces, threads=threads)
+            ts_.append((time.perf_counter() - t0) * 1e3)
+        out[name] = statistics.median(ts_)
+    out["per_node_dkg_ms"] = out["part_rows_ms"] + n_nodes * out["ack_values_ms"]
+    out["encryptions_per_node"] = n_nodes + n_nodes * n_nodes
+    out["host_threads"] = threads
+    out["note"] = ("host stage, %d threads; one Part = %d row encryptions, one Ack = %d value encryptions; "
+                   "per_node_dkg_ms = one Part + %d Acks" % (threads, n_nodes, n_nodes, n_nodes))
+    return out
+
+
+def g1a_abi():
+    from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
+    return g1a(G1_UNC)
 
 
 def cpu_baseline_dkg(t, parts, pidx, xs, ys, vals, expected, eng, per_thread=16):
@@ -1014,7 +1093,7 @@ def run_pool(args):
         dsh = gen.g1_mul([us[w.doc_idx[i]] for i in range(n)],
                          [rng.randrange(1, R_ORDER) if i in set(bad) else w.sk[w.node[i]] for i in range(n)])
         ins = [b"".join(dsh) * nsh, w.pk_batch * nsh, w.hash_table * nsh, b"".join(ws) * nsh]
-        fn_name, kernel, op, unit_name = ("hbh_verify_dec_shares", "hbs::k_pair_verify<false, false, 0>",
+        fn_name, kernel, op, unit_name = ("hbh_verify_dec_shares", KERNEL_NAMES["decrypt"],
                                           workcount.PAIR_CHECK_TABLE, "decryption-share check")
     gen.close()
     pool = Pool(devs)

@@ -214,16 +214,18 @@ HP_D H6 h6_neg(const H6& a) { return {fp_neg(a.c0), fp_neg(a.c1), fp_neg(a.c2)};
 HP_D H6 h6_red(const H6& a) { return {fp_reduce(a.c0), fp_reduce(a.c1), fp_reduce(a.c2)}; }
 HP_D H6 h6_mul_v(const H6& a) { return {h_mul_xi(a.c2), a.c0, a.c1}; }
 
-// Karatsuba, inputs < 4p
+// Karatsuba, inputs < 4p; outputs reduced (one carry pass each, fp_red_l).  Register-frugal order:
+// each output is formed as soon as its products exist (c0 before t1, t2 are computed), so at most
+// five Fp2 values are live beside the operands across the product calls.
 HP_D H6 h6_mul(const H6& a, const H6& b) {
-  const Fp v0 = h_mul(a.c0, b.c0);
   const Fp v1 = h_mul(a.c1, b.c1);
   const Fp v2 = h_mul(a.c2, b.c2);
-  const Fp t0 = h_mul(fp_addl(a.c1, a.c2), fp_add(b.c1, b.c2));
-  const Fp t1 = h_mul(fp_addl(a.c0, a.c1), fp_add(b.c0, b.c1));
-  const Fp t2 = h_mul(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2));
-  return {fp_add(v0, h_mul_xi(fp_sub(fp_subl(t0, v1), v2))), fp_add(fp_sub(fp_subl(t1, v0), v1), h_mul_xi(v2)),
-          fp_add(fp_sub(fp_subl(t2, v0), v2), v1)};
+  const Fp d0 = fp_sub2l(h_mul(fp_addl(a.c1, a.c2), fp_add(b.c1, b.c2)), v1, v2);
+  const Fp v0 = h_mul(a.c0, b.c0);
+  const Fp c0 = fp_red_l(h_add_xi_l(v0, d0));  // v0 + xi (t0 - v1 - v2)
+  const Fp c1 = fp_red_l(h_add_xi_l(fp_sub2l(h_mul(fp_addl(a.c0, a.c1), fp_add(b.c0, b.c1)), v0, v1), v2));
+  const Fp c2 = fp_red_l(fp_addl(fp_sub2l(h_mul(fp_addl(a.c0, a.c2), fp_add(b.c0, b.c2)), v0, v2), v1));
+  return {c0, c1, c2};
 }
 // x (a + b v)
 HP_D H6 h6_mul_01(const H6& x, const Fp& a, const Fp& b) {
@@ -269,13 +271,15 @@ HP_D H12 h12_mul(const H12& a, const H12& b) {
   const H6 t0 = h6_mul(a.c0, b.c0);
   const H6 t1 = h6_mul(a.c1, b.c1);
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_add(b.c0, b.c1));
-  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
+  return h12_kcomb(t0, t1, s);
 }
-// complex squaring
+// complex squaring: t = a0 a1, s = (a0 + a1)(a0 + v a1); c0 = s - t - v t, c1 = 2 t (one pass each)
 HP_D H12 h12_sqr(const H12& a) {
-  const H6 t = h6_red(h6_mul(a.c0, a.c1));
+  const H6 t = h6_mul(a.c0, a.c1);
   const H6 s = h6_mul(h6_add(a.c0, a.c1), h6_red(h6_add(a.c0, h6_mul_v(a.c1))));
-  return h12_red({h6_sub(h6_sub(s, t), h6_mul_v(t)), h6_add(t, t)});
+  return {{fp_red_l(h_add_xi_l(fp_subl(s.c0, t.c0), fp_subl(fp_zero(), t.c2))), fp_red_l(fp_sub2l(s.c1, t.c1, t.c0)),
+           fp_red_l(fp_sub2l(s.c2, t.c2, t.c1))},
+          {fp_red_l(fp_addl(t.c0, t.c0)), fp_red_l(fp_addl(t.c1, t.c1)), fp_red_l(fp_addl(t.c2, t.c2))}};
 }
 // f (c0 + c1 w^2 + c4 w^3); c0, c1, c4 normalised, < 2p
 HP_D H12 h12_mul_014(const H12& f, const Fp& c0, const Fp& c1, const Fp& c4) {
@@ -286,14 +290,15 @@ HP_D H12 h12_mul_014(const H12& f, const Fp& c0, const Fp& c1, const Fp& c4) {
   const H6 s = h6_red(h6_mul_01(fs, c0, c14));
   return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
 }
-// x (b1 v + b2 v^2): c0 = xi (a1 b2 + a2 b1), c1 = a0 b1 + xi a2 b2, c2 = a0 b2 + a1 b1 (5 products)
+// x (b1 v + b2 v^2): c0 = xi (a1 b2 + a2 b1), c1 = a0 b1 + xi a2 b2, c2 = a0 b2 + a1 b1 (5 products);
+// outputs reduced
 HP_D H6 h6_mul_12(const H6& x, const Fp& b1, const Fp& b2) {
   const Fp u = h_mul(x.c1, b1);
   const Fp w = h_mul(x.c2, b2);
-  const Fp z = fp_sub(fp_subl(h_mul(fp_addl(x.c1, x.c2), fp_add(b1, b2)), u), w);
-  const Fp p = h_mul(x.c0, b1);
-  const Fp q = h_mul(x.c0, b2);
-  return {h_mul_xi(z), fp_add(p, h_mul_xi(w)), fp_add(q, u)};
+  const Fp c0 = fp_red_l(h_xi_l(fp_sub2l(h_mul(fp_addl(x.c1, x.c2), fp_add(b1, b2)), u, w)));
+  const Fp c1 = fp_red_l(h_add_xi_l(h_mul(x.c0, b1), w));
+  const Fp c2 = fp_red_l(fp_addl(h_mul(x.c0, b2), u));
+  return {c0, c1, c2};
 }
 // f * (la * lb) for two sparse lines (c0 + c1 w^2 + c4 w^3 each, normalised, < 2p): the line
 // product L = (C0, C1) has C1.c0 = 0 (6 products), then one Karatsuba step with the sparse C1
@@ -303,15 +308,16 @@ HP_D H12 h12_mul_lines(const H12& f, const Fp& a0, const Fp& a1, const Fp& a4, c
   const Fp a0b0 = h_mul(a0, b0);
   const Fp a1b1 = h_mul(a1, b1);
   const Fp a4b4 = h_mul(a4, b4);
-  const Fp x1 = fp_sub(fp_subl(h_mul(fp_addl(a0, a1), fp_add(b0, b1)), a0b0), a1b1);
-  const Fp y1 = fp_sub(fp_subl(h_mul(fp_addl(a0, a4), fp_add(b0, b4)), a0b0), a4b4);
-  const Fp y2 = fp_sub(fp_subl(h_mul(fp_addl(a1, a4), fp_add(b1, b4)), a1b1), a4b4);
-  const H6 C0 = h6_red({fp_add(a0b0, h_mul_xi(a4b4)), x1, a1b1});
-  const Fp c11 = fp_reduce(y1), c12 = fp_reduce(y2);
-  const H6 t0 = h6_red(h6_mul(f.c0, C0));
-  const H6 t1 = h6_red(h6_mul_12(f.c1, c11, c12));
-  const H6 s = h6_red(h6_mul(h6_add(f.c0, f.c1), h6_red({C0.c0, fp_add(C0.c1, c11), fp_add(C0.c2, c12)})));
-  return h12_red({h6_add(t0, h6_mul_v(t1)), h6_sub(h6_sub(s, t0), t1)});
+  // the line product L = (C0, (0, c11, c12)), each coefficient reduced in one carry pass
+  const Fp c11 = fp_red_l(fp_sub2l(h_mul(fp_addl(a0, a4), fp_add(b0, b4)), a0b0, a4b4));
+  const Fp c12 = fp_red_l(fp_sub2l(h_mul(fp_addl(a1, a4), fp_add(b1, b4)), a1b1, a4b4));
+  const H6 C0 = {fp_red_l(h_add_xi_l(a0b0, a4b4)),
+                 fp_red_l(fp_sub2l(h_mul(fp_addl(a0, a1), fp_add(b0, b1)), a0b0, a1b1)), a1b1};
+  // f L: Karatsuba over Fp6 with the sparse L.c1 (6 + 5 + 6 products); h6_mul / h6_mul_12 reduce
+  const H6 t0 = h6_mul(f.c0, C0);
+  const H6 t1 = h6_mul_12(f.c1, c11, c12);
+  const H6 s = h6_mul(h6_add(f.c0, f.c1), {C0.c0, fp_add(C0.c1, c11), fp_add(C0.c2, c12)});
+  return h12_kcomb(t0, t1, s);
 }
 HP_D H12 h12_inv(const H12& a) {
   const H6 t = h6_red(h6_sub(h6_red(h6_mul(a.c0, a.c0)), h6_red(h6_mul_v(h6_red(h6_mul(a.c1, a.c1))))));

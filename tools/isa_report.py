@@ -100,3 +100,19 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def loop_head(path, kernel, loop_start):
+    """Instructions of a loop from its start to the first conditional branch (the unconditional hot
+    part, e.g. the squaring of a square-and-multiply loop)."""
+    funcs = parse(disasm(path))
+    for name, (base, ins) in funcs.items():
+        if kernel in name:
+            body = []
+            for a, op, l in ins:
+                if a - base < loop_start:
+                    continue
+                body.append((a, op, l))
+                if op.startswith("s_cbranch"):
+                    break
+            return summary(body)
