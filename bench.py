@@ -45,14 +45,12 @@ MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
 IMPLS = {"auto": 3, "pair": 4, "wave": 5}   # HBH_IMPL_* (include/hbbft_hip.h)
-# the lane-pair check runs as three kernels (csrc/k_pair.hip: lines, f, final exponentiation); its
-# roofline entry is the whole pairing stage, and its traffic the three kernels' sum
-PAIR_SIGN = ("hbs::k_pair_lines<false, true, 2>", "hbs::k_pair_f", "hbs::k_pair_fe")
-PAIR_DECRYPT = ("hbs::k_pair_lines<false, false, 0>", "hbs::k_pair_f", "hbs::k_pair_fe")
-KERNEL_NAMES = {"pair": " + ".join(PAIR_SIGN),
+PAIR_SIGN = "hbs::k_pair_verify<false, true, 2>"
+PAIR_DECRYPT = "hbs::k_pair_verify<false, false, 0>"
+KERNEL_NAMES = {"pair": PAIR_SIGN,
                 "wave": "hbs::k_wave (one wave per check)",
-                "auto": " + ".join(PAIR_SIGN),
-                "decrypt": " + ".join(PAIR_DECRYPT)}
+                "auto": PAIR_SIGN,
+                "decrypt": PAIR_DECRYPT}
 G1_UNC = bytes.fromhex(
     "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
     "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
@@ -261,7 +259,7 @@ def reference_work(main_k, workcount):
 
 
 def pair_waves_per_simd(checks):
-    """The lane-pair kernels (k_pair_lines / k_pair_f / k_pair_fe): two lanes per check, 64-lane waves, 1,024 SIMDs."""
+    """The lane-pair kernel k_pair_verify: two lanes per check, 64-lane waves, 1,024 SIMDs."""
     w = checks * 2 / 64 / 1024
     return 2 if w >= 2 else (1 if w >= 1 else round(w, 3))
 
@@ -439,6 +437,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
     ap.add_argument("--impl", choices=["pair", "wave", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
+    ap.add_argument("--profile-epoch", default=None, metavar="FILE",
+                    help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
     ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
     ap.add_argument("--epoch-coins", choices=["ba", "synthetic"], default="ba",
                     help="epoch workload: coins from Binary Agreement instances or one ThresholdSign each")
@@ -449,8 +449,12 @@ def main():
     ap.add_argument("--dkg-scope", choices=["network", "node"], default="network",
                     help="dkg workload: the whole network's 10^6 ack checks split over the ranks, or one node's "
                          "10,000 per rank")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="epoch workload: drain each window before handling it (no GPU/host overlap)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="epoch workload: drain window k on a worker thread while the flows handle window k - 1 "
+                         "(measured slower than serial drains on MI355X, profiles/r04/c6_epoch_ab.txt)")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="epoch workload: no next-epoch coin prefetch (hash and sign every coin document in "
+                         "its own epoch)")
     ap.add_argument("--launcher", choices=["ranks", "pool"], default="ranks",
                     help="--gpus N > 1 without torchrun: spawn N ranks (one process per GPU, default) or drive "
                          "the in-ABI engine pool (hbh_pool_*) over N devices from this process")
@@ -956,32 +960,61 @@ def run_epoch_bench(args, eng, world, rank, dev):
     the mirrored flows with windowed drains and batched combines.  One step = one epoch (a fresh
     trace each); every rank plays its own node (weak scaling, no collective)."""
     from hbbft_amd import workcount
-    from hbbft_amd._lib import STAGE_PAIRING
-    from hbbft_amd.honey_badger import EpochTrace, NetworkKeys, run_epoch
+    from hbbft_amd._lib import STAGE_CURVE, STAGE_PAIRING, STAGE_PREPARE
+    from hbbft_amd.honey_badger import EpochTrace, NetworkKeys, prefetch_coins, run_epoch
     rng = random.Random(5000 + rank)
     n, f = 100, 33
     keys = NetworkKeys(eng, n, f, rng)
     t0 = time.time()
-    traces = [EpochTrace.generate(eng, keys, rng, hb_epoch=e, proposal_bytes=1000) for e in range(args.warmup + args.steps)]
+    # one trace beyond the timed epochs: the last timed epoch prefetches its coin documents
+    traces = [EpochTrace.generate(eng, keys, rng, hb_epoch=e, proposal_bytes=1000)
+              for e in range(args.warmup + args.steps + 1)]
     if args.epoch_coins == "ba":  # coins from Binary Agreement instances (future-epoch queue, per-window combines)
         for tr in traces:
             tr.with_ba(eng, rng, extra=0.0)
     log("generated %d epoch traces in %.1f s" % (len(traces), time.time() - t0))
     ok = True
-    for tr in traces[:args.warmup]:
-        r = run_epoch(eng, keys, tr, window=args.window, pipelined=not args.no_pipeline)
+    # each epoch starts the next one's coin prefetch (honey_badger.prefetch_coins: hash_g2 and our
+    # share of the next epoch's BA coin documents, on the host-stage thread); the timed region
+    # waits for the prefetch the last timed epoch started, so every timed epoch carries one
+    pf_on = args.epoch_coins == "ba" and not args.no_prefetch
+
+    def prefetch(k):
+        return prefetch_coins(keys, traces[k].hb_epoch, range(n)) if pf_on else None
+
+    pf = prefetch(0)
+    for k, tr in enumerate(traces[:args.warmup]):
+        nxt = prefetch(k + 1)
+        r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf)
+        pf = nxt
         ok = ok and r.plaintexts == tr.proposals
     if world > 1:
         dist.barrier()
     results = []
     eng.set_profiling(True)
+    prof = None
+    if args.profile_epoch:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
-    for tr in traces[args.warmup:]:
-        results.append(run_epoch(eng, keys, tr, window=args.window, pipelined=not args.no_pipeline))
+    for k in range(args.warmup, len(traces) - 1):
+        nxt = prefetch(k + 1)
+        results.append(run_epoch(eng, keys, traces[k], window=args.window, pipelined=args.pipeline, coin_prefetch=pf))
+        pf = nxt
+    if pf is not None:
+        pf.result()
     wall = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        with open(args.profile_epoch, "w") as fh:
+            pstats.Stats(prof, stream=fh).sort_stats("tottime").print_stats(45)
     pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
+    stage_ms = {name: eng.stage_time(st)[0] for name, st in
+                (("line_tables", STAGE_PREPARE), ("pairing", STAGE_PAIRING), ("curve", STAGE_CURVE))}
     eng.set_profiling(False)
-    for tr, r in zip(traces[args.warmup:], results):
+    for tr, r in zip(traces[args.warmup:-1], results):
         ok = ok and r.plaintexts == tr.proposals and len(r.coins) == len(tr.coin_docs)
         if args.epoch_coins == "ba":
             ok = ok and r.ba_decisions == tr.ba.decision and r.ba_coins == tr.ba.coins
@@ -990,6 +1023,14 @@ def run_epoch_bench(args, eng, world, rank, dev):
         drained = sum(r.checks_gpu for r in results)
         consumed = sum(r.checks_consumed for r in results) / len(results)
         phases = {k: sum(r.timing[k] for r in results) / len(results) * 1e3 for k in results[0].timing}
+        waits = {k: sum(r.wait.get(k, 0.0) for r in results) / len(results) * 1e3 for k in results[0].wait}
+        kern = {k: v / len(results) for k, v in stage_ms.items()}
+        # host time = the epoch minus the time the flows sat blocked on engine calls (GPU kernels,
+        # copies and the engine's own host work); the kernels' own time is the event-timed stages
+        host_gpu = {"epoch_ms": phases["epoch"], "blocked_on_engine_ms": sum(waits.values()),
+                    "host_ms": phases["epoch"] - sum(waits.values()), "gpu_kernel_ms": sum(kern.values()),
+                    "blocked_by_phase_ms": waits, "gpu_kernel_by_stage_ms": kern}
+        host_gpu["host_over_gpu"] = host_gpu["host_ms"] / max(host_gpu["gpu_kernel_ms"], 1e-9)
         # AUTO sends drains of <= HBH_AUTO_WAVE_MAX checks (all of an epoch's) to the wave kernel.
         main_k = roofline_entry("hbs::k_wave", pair_n, pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
                                 workcount.PAIR_CHECK_WALK, "share / ciphertext check")
@@ -1004,10 +1045,11 @@ def run_epoch_bench(args, eng, world, rank, dev):
                        "coins_from": ("BinaryAgreementCoin instances (epochs 0-2, coin shares through the future-epoch "
                                       "queue, combines deferred per window)" if args.epoch_coins == "ba"
                                       else "synthetic: one ThresholdSign per BA instance at epoch 2"),
-                       "pipelined_drains": not args.no_pipeline,
+                       "pipelined_drains": args.pipeline,
+                       "coin_prefetch": pf_on,
                        "parallelism": "one node per rank x%d" % world,
                        "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},
-            "outputs_ok": ok, "phase_ms": phases,
+            "outputs_ok": ok, "phase_ms": phases, "host_vs_gpu": host_gpu,
             "engine_calls_per_epoch": sum(r.engine_calls for r in results) / len(results),
             "checks_drained_per_epoch": drained / len(results), "checks_consumed_per_epoch": consumed,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)", traffic=None,

@@ -24,6 +24,7 @@ The CPU comparison is the reference-equivalent work: the checks the flows actual
 (``BatchVerifier.lookups``: shares that arrived before their instance terminated) plus the
 combines, timed on the C restatement by bench.py (oracle use stays in bench/tests).
 """
+import concurrent.futures
 import random
 import struct
 import sys
@@ -190,6 +191,7 @@ def _serialize(trace, corrupt=()):
 EpochTrace.serialize = _serialize
 
 BOTH = frozenset((False, True))
+_EMPTY = Step()  # the Step of a message to a terminated instance: read by the drivers, never extended
 
 
 class BaTrace:
@@ -278,6 +280,7 @@ class EpochResult:
         self.checks_gpu = 0    # checks drained through the engine (incl. post-termination window tail)
         self.checks_consumed = 0  # verdicts the flows used (the reference's per-message checks)
         self.combines = 0
+        self.wait = {}          # phase -> seconds the flows spent blocked on engine calls
         self.ba_decisions = {}  # proposer -> BA decision (BA-driven coins)
         self.ba_coins = {}      # proposer -> {BA epoch: threshold coin}
         self.ba_queued = 0      # coin shares that waited in a BA future-epoch queue
@@ -342,8 +345,8 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
         yield from hand(prev)
 
 
-def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True, slack=4, switch_interval=2e-4,
-              defer=True, raw=False, ba=None):
+def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
+              defer=True, raw=False, ba=None, coin_prefetch=None):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
     ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
@@ -364,7 +367,7 @@ def run_epoch(engine, keys, trace, window=4096, our=0, threads=0, pipelined=True
     if pipelined and switch_interval:
         sys.setswitchinterval(switch_interval)
     try:
-        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba)
+        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch)
     finally:
         sys.setswitchinterval(old)
 
@@ -383,9 +386,58 @@ def _decoder(engine, raw_msgs, out, fn):
     return decode
 
 
-def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba):
+_HOST = None  # one worker for host-stage crypto that overlaps the flows (ctypes calls release the GIL)
+
+
+def _host_pool():
+    global _HOST
+    if _HOST is None:
+        _HOST = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="hbh-host")
+    return _HOST
+
+
+def _decrypt_prep(cts, sk, threads):
+    """The host work of a contribution that depends only on its ciphertext bytes: H_uv =
+    hash_g1_g2(U, V) (Ciphertext::verify's and every share check's hash) and our own decryption
+    share U * sk (threshold_decrypt.rs:164).  RBC delivers a contribution before the BA instances and
+    the Subset decide (src/honey_badger/epoch_state.rs: decryption starts at the Subset output), so
+    this runs on a host thread from the start of the epoch, beside the coin phase; the threshold
+    decryption itself still starts at the Subset output."""
+    ps = sorted(cts)
+    if not ps:
+        return {}, {}
+    huv = hoststage.hash_g1_g2([cts[p][0] for p in ps], [cts[p][1] for p in ps], threads=threads)
+    own = hoststage.g1_mul([cts[p][0] for p in ps], [sk] * len(ps), threads=threads)
+    return dict(zip(ps, huv)), dict(zip(ps, own))
+
+
+def prefetch_coins(keys, hb_epoch, proposers, our=0, ba_epochs=(2,), hb_id=0, threads=0):
+    """Start hashing the threshold-coin documents of a LATER HoneyBadger epoch and signing our
+    shares on them, on the host-stage thread, while the current epoch runs.  A coin document is
+    bincode((hb_id, hb_epoch, proposer), ba_epoch) (binary_agreement.rs:442; subset.rs:182-185), so
+    the next epoch's first threshold coins (BA epoch 2 of every proposer's instance) are known before
+    that epoch starts; the reference hashes and signs each when its Conf round completes
+    (threshold_sign.rs:151, 176) -- same values, computed earlier.  Returns a future of
+    {document: (hash_g2(document), our share)} for run_epoch(..., coin_prefetch=)."""
+    docs = [coin_document(hb_id, hb_epoch, p, e) for p in proposers for e in ba_epochs]
+    sk = keys.sks[our]
+    bg = threads if threads else max(1, hoststage.host_threads() - 2)
+
+    def job():
+        if not docs:
+            return {}
+        hs = hoststage.hash_g2(docs, threads=bg)
+        sigs = hoststage.g2_mul(hs, [sk] * len(hs), threads=bg)
+        return {d: (h, g) for d, h, g in zip(docs, hs, sigs)}
+    return _host_pool().submit(job)
+
+
+def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
+    # the background host work leaves two of the host threads to the flows and the drain worker
+    bg = threads if threads else max(1, hoststage.host_threads() - 2)
+    prep = None if raw else _host_pool().submit(_decrypt_prep, trace.cts, keys.sks[our], bg)
     ver = BatchVerifier(engine)
     ver.recording = defer                  # combines of the epoch run in one batch at the end
     sk = keys.sks[our]
@@ -395,20 +447,21 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     # --- Binary Agreement coins: ThresholdSign per BA instance that reaches a coin epoch
     t0 = time.perf_counter()
     if ba:
-        coin_out = _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res)
+        coin_out = _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined, coin_prefetch)
         coin_sh, dec_sh = ({}, {}) if raw else (trace.coin_shares, trace.dec_shares)
         handed = {}
         ni_sign = None
         ts = {}
         res.timing["coin_verify"] = time.perf_counter() - t0
+        res.wait["coin"] = ver.wait_s
     else:
         coin_out, handed, ni_sign, ts, coin_sh, dec_sh = _coins(engine, keys, trace, ver, window, our, threads,
                                                                pipelined, limit, res, raw, sk, n, t0)
     return _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n,
-                               t_all, coin_out, handed, ni_sign, ts, coin_sh, dec_sh)
+                               t_all, coin_out, handed, ni_sign, ts, coin_sh, dec_sh, prep)
 
 
-def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
+def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined=False, coin_prefetch=None):
     """The BA-driven coin phase: one BinaryAgreementCoin per proposer with a coin (trace.ba).
     Messages (p, e, j) come in windows; before a window's drain, every share of a running or
     FUTURE epoch of its instance is queued (coin documents are hashed when first seen; a future
@@ -424,13 +477,24 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
     ni = NetworkInfo(our, range(keys.n), keys.t, keys.master_pk, keys.pks, sign_g2=lambda H: own_sig[bytes(H)])
     # our own shares: one batched host signing for every coin document on the instances' paths
     # (the reference signs each when its Conf round completes; the share is the same)
+    t0 = time.perf_counter()
     pe = sorted(ba.docs)
-    ver.hash_docs([ba.docs[k] for k in pe])  # one threaded host-stage call for every coin document
+    ready = coin_prefetch.result() if coin_prefetch is not None else {}  # (hash, our share) per document
+    ver.add_doc_hashes({bytes(ba.docs[k]): ready[bytes(ba.docs[k])][0] for k in pe if bytes(ba.docs[k]) in ready})
+    ver.hash_docs([ba.docs[k] for k in pe])  # one threaded host-stage call for the documents not prefetched
     hs = [ver.doc_hash_of(ba.docs[k]) for k in pe]
     hmap = dict(zip(pe, hs))
-    for h, sgn in zip(hs, hoststage.g2_mul(hs, [sk] * len(hs), threads=threads) if hs else []):
+    res.timing["coin_hash"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    todo = [h for k, h in zip(pe, hs) if bytes(ba.docs[k]) not in ready]
+    for h, sgn in zip(todo, hoststage.g2_mul(todo, [sk] * len(todo), threads=threads) if todo else []):
         own_sig[bytes(h)] = sgn
-        ver.queue_sig(keys.pks[our], h, sgn)
+    for k, h in zip(pe, hs):
+        d = bytes(ba.docs[k])
+        if d in ready:
+            own_sig[bytes(h)] = ready[d][1]
+        ver.queue_sig(keys.pks[our], h, own_sig[bytes(h)])
+    res.timing["coin_own_shares"] = time.perf_counter() - t0
     bas = {p: BinaryAgreementCoin(ni, ver, (hb_id, trace.hb_epoch, p)) for p in sorted(ba.sched)}
     fired = set()
     queued_n = {}
@@ -473,11 +537,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
                     except ProtocolError as err:
                         res.errors.append(("coin", p, err))
 
-    local_events(0)
-    resolve()
-    msgs = ba.msgs
-    for w0 in range(0, len(msgs), window):
-        batch = msgs[w0:w0 + window]
+    def queue_window(batch):
         for p, e, j in batch:
             b = bas[p]
             if b.decision is None and e >= b.epoch and (b.epoch < e or not b.coin_decided):
@@ -488,15 +548,41 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res):
                 if limit is None or c < limit or e > b.epoch:
                     ver.queue_sig(keys.pks[j], hmap[(p, e)], ba.shares[(p, e, j)])
                     queued_n[(p, e)] = c + 1
-        ver.drain()
+
+    def hand_window(batch, end):
         for p, e, j in batch:
+            b = bas[p]
+            if b.decision is not None:  # a decided instance ignores every message (:245-248)
+                continue
             try:
-                record(p, bas[p].handle_message(j, e, ba.shares[(p, e, j)]))
+                record(p, b.handle_message(j, e, ba.shares[(p, e, j)]))
             except ProtocolError as err:
                 res.errors.append(("coin", p, err))
         resolve()
-        local_events(w0 + len(batch))
+        local_events(end)
         resolve()
+
+    local_events(0)
+    resolve()
+    msgs = ba.msgs
+    # pipelined (as _deliver): window k's checks are queued from the state before window k - 1 is
+    # handled and drained on the GPU while the host handles window k - 1 -- a few checks of instances
+    # that decide in window k - 1 may be drained unread; verdicts are pure, the Steps are the serial ones
+    prev = None
+    for w0 in range(0, len(msgs), window):
+        batch = msgs[w0:w0 + window]
+        queue_window(batch)
+        if not pipelined:
+            ver.drain()
+            hand_window(batch, w0 + len(batch))
+            continue
+        pending = ver.drain_async()
+        if prev is not None:
+            hand_window(*prev)
+        ver.commit(pending)
+        prev = (batch, w0 + len(batch))
+    if prev is not None:
+        hand_window(*prev)
     local_events(len(msgs) + 1)
     resolve()
     out = {}
@@ -535,7 +621,10 @@ def _coins(engine, keys, trace, ver, window, our, threads, pipelined, limit, res
 
     def hand_coin(p, j):
         handed.setdefault(("coin", p), []).append(j)
-        return ts[p].handle_message(j, coin_sh[(p, j)])
+        inst = ts[p]
+        if inst.terminated:
+            return _EMPTY
+        return inst.handle_message(j, coin_sh[(p, j)])
 
     for p, out in _deliver(ver, trace.coin_msgs, window, ts,
                            lambda p, j: ver.queue_sig(keys.pks[j], ts[p].doc_hash, coin_sh[(p, j)]),
@@ -543,11 +632,12 @@ def _coins(engine, keys, trace, ver, window, our, threads, pipelined, limit, res
                            _decoder(engine, trace.raw_coin, coin_sh, wire.decode_sig_share_msgs) if raw else None):
         coin_out[p] = out
     res.timing["coin_verify"] = time.perf_counter() - t0
+    res.wait["coin"] = ver.wait_s
     return coin_out, handed, ni_sign, ts, coin_sh, dec_sh
 
 
 def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n, t_all,
-                        coin_out, handed, ni_sign, ts, coin_sh, dec_sh):
+                        coin_out, handed, ni_sign, ts, coin_sh, dec_sh, prep=None):
     # --- Subset output: the N ciphertexts into ThresholdDecrypt
     t0 = time.perf_counter()
     ps = sorted(trace.cts)
@@ -557,9 +647,14 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
         ps = [p for p in ps if got[p] is not None]
     else:
         got = trace.cts
-    huv = hoststage.hash_g1_g2([got[p][0] for p in ps], [got[p][1] for p in ps], threads=threads) if ps else []
+    if prep is not None:  # hashed and our shares computed beside the coin phase (_decrypt_prep)
+        huv_of, own_of = prep.result()
+        huv = [huv_of[p] for p in ps]
+        own_dec = {p: own_of[p] for p in ps}
+    else:
+        huv = hoststage.hash_g1_g2([got[p][0] for p in ps], [got[p][1] for p in ps], threads=threads) if ps else []
+        own_dec = dict(zip(ps, hoststage.g1_mul([got[p][0] for p in ps], [sk] * len(ps), threads=threads)))
     cts = {p: Ciphertext(got[p][0], got[p][1], got[p][2], h) for p, h in zip(ps, huv)}
-    own_dec = dict(zip(ps, hoststage.g1_mul([cts[p].u for p in ps], [sk] * len(ps), threads=threads)))
     by_u = {cts[p].u: own_dec[p] for p in ps}
     ni_dec = NetworkInfo(our, range(n), keys.t, keys.master_pk, keys.pks, decrypt_share=lambda U: by_u[bytes(U)])
     td = {p: ThresholdDecrypt(ni_dec, ver) for p in ps}
@@ -586,7 +681,10 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
 
     def hand_dec(p, j):
         handed.setdefault(("dec", p), []).append(j)
-        return td[p].handle_message(j, dec_sh[(p, j)])
+        inst = td[p]
+        if inst.terminated:  # handle_message of a terminated instance is an empty Step (:183-185)
+            return _EMPTY
+        return inst.handle_message(j, dec_sh[(p, j)])
 
     dec_msgs = [m for m in trace.dec_msgs if m[0] in td]  # (shares of a faulted contribution: no instance)
     for p, out in _deliver(ver, dec_msgs, window, td,
@@ -595,11 +693,13 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
                            _decoder(engine, trace.raw_dec, dec_sh, wire.decode_dec_share_msgs) if raw else None):
         dec_out[p] = out
     res.timing["decrypt_verify"] = time.perf_counter() - t0
+    res.wait["decrypt"] = ver.wait_s - res.wait.get("coin", 0.0)
 
     # --- deferred combines: one G2 combine+verify batch, one G1 interpolation batch
     t0 = time.perf_counter()
     failed = {id(d) for d in ver.flush_combines()}
     res.timing["combine"] = time.perf_counter() - t0
+    res.wait["combine"] = ver.wait_s - res.wait.get("coin", 0.0) - res.wait["decrypt"]
     t0 = time.perf_counter()
     # A failed deferred combine: the reference returned Err from the call that triggered it (and a
     # ThresholdSign stayed open), so that instance is replayed with immediate combines; its Steps

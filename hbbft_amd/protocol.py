@@ -15,6 +15,7 @@ What stays on the host, as in the reference and the north star: hashing to G2 (`
 ``PublicKeySet::decrypt`` -- all through the product host stage (``hbbft_amd.hoststage``, C++).
 """
 import concurrent.futures
+import time
 
 from . import hoststage
 from ._lib import G1_BYTES, G2_BYTES
@@ -35,11 +36,14 @@ class Fault:
 
 class Step:
     """``Step { output, fault_log, messages }``; messages are (target, payload), target "all"."""
+    __slots__ = ("output", "fault_log", "messages")
 
     def __init__(self, output=None, fault_log=None, messages=None):
-        self.output = list(output or [])
-        self.fault_log = list(fault_log or [])
-        self.messages = list(messages or [])
+        # the flows create ~30,000 Steps per epoch: no copies of the caller's lists (callers pass
+        # fresh lists) and no per-instance dict
+        self.output = [] if output is None else output
+        self.fault_log = [] if fault_log is None else fault_log
+        self.messages = [] if messages is None else messages
 
     @staticmethod
     def fault(node_id, kind):
@@ -144,6 +148,7 @@ class BatchVerifier:
         self._released = set()  # instances released since the last drain was stored
         self._open = {}         # instance key -> number of running instances that use it
         self._inflight = 0      # drain_async calls not yet committed
+        self.wait_s = 0.0       # time the calling thread spent blocked on engine calls (drains, combines)
 
     # -------------------------------------------------------------- host hashing
     def hash_docs(self, docs):
@@ -151,6 +156,12 @@ class BatchVerifier:
         docs = [bytes(d) for d in docs if bytes(d) not in self._docs]
         for d, h in zip(docs, hoststage.hash_g2(docs) if docs else []):
             self._docs[d] = h
+
+    def add_doc_hashes(self, hashes):
+        """Documents hashed elsewhere ({document: hash_g2(document)}, e.g. prefetched by
+        honey_badger.prefetch_coins) into the hash_docs cache."""
+        for d, h in hashes.items():
+            self._docs.setdefault(bytes(d), h)
 
     def hash_doc(self, doc):
         doc = bytes(doc)
@@ -175,7 +186,9 @@ class BatchVerifier:
             d = Deferred(key)
             self._rec_g2.append(d)
             return d, 0, True
+        t0 = time.perf_counter()
         out, st, v = self.eng.combine_verify_g2(t, [list(idx)], [list(shares)], master_pk, [h])
+        self.wait_s += time.perf_counter() - t0
         self.calls += 1
         return out[0], st[0], bool(v[0])
 
@@ -186,13 +199,16 @@ class BatchVerifier:
             d = Deferred(key)
             self._rec_g1.append(d)
             return d, 0
+        t0 = time.perf_counter()
         out, st = self.eng.interpolate_g1(t, [list(idx)], [list(shares)])
+        self.wait_s += time.perf_counter() - t0
         self.calls += 1
         return out[0], st[0]
 
     def flush_combines(self):
         """Run every deferred combine: one engine call per (t, master key) for G2 and per t for G1;
         fills each Deferred's result; returns the Deferreds whose combine failed."""
+        t0 = time.perf_counter()
         groups = {}
         for d in self._rec_g2:
             groups.setdefault((d.key[0], d.key[3]), []).append(d)
@@ -210,6 +226,7 @@ class BatchVerifier:
             self.calls += 1
             for d, o, s_ in zip(ds, out, st):
                 d.result = (o, s_)
+        self.wait_s += time.perf_counter() - t0
         failed = [d for d in self._rec_g2 + self._rec_g1 if not d.ok]
         self._rec_g2, self._rec_g1 = [], []
         return failed
@@ -274,7 +291,7 @@ class BatchVerifier:
         v = self._sig.get(h, {}).get(k)
         if v is None:
             self._qsig.append((k[0], h, k[1]))
-            v = self.drain()[("sig", h, k)]
+            v = self._drain(("sig", h, k))
         return v
 
     # ThresholdDecrypt: PublicKeyShare::verify_decryption_share(share, ct)  (src/threshold_decrypt.rs:227)
@@ -289,7 +306,7 @@ class BatchVerifier:
         v = self._dec.get(c, {}).get(k)
         if v is None:
             self._qdec.append(k + c)
-            v = self.drain()[("dec", c, k)]
+            v = self._drain(("dec", c, k))
         return v
 
     # Ciphertext::verify  (src/threshold_decrypt.rs:142)
@@ -304,14 +321,23 @@ class BatchVerifier:
         v = self._ct.get(c, {}).get(u)
         if v is None:
             self._qct.append((u, c[1], c[0]))
-            v = self.drain()[("ct", c, u)]
+            v = self._drain(("ct", c, u))
         return v
 
     def drain(self):
-        """Verify everything queued: one engine call per kind.  Returns the fresh verdicts by
-        (kind, instance key, item key) -- a synchronous *_valid reads its verdict from there even
-        when no running instance keeps it cached."""
-        return self._store(self._run_jobs(self._take_jobs()))
+        """Verify everything queued: one engine call per kind."""
+        self._drain(None)
+
+    def _drain(self, want):
+        jobs = self._take_jobs()
+        if not jobs:
+            if not self._inflight:
+                self._released.clear()
+            return None
+        t0 = time.perf_counter()
+        res = self._run_jobs(jobs)
+        self.wait_s += time.perf_counter() - t0
+        return self._store(res, want)
 
     def drain_async(self):
         """Start verifying everything queued on a worker thread (one engine call per kind, the
@@ -327,11 +353,13 @@ class BatchVerifier:
 
     def commit(self, pending):
         """Wait for a ``drain_async`` and cache its verdicts."""
+        t0 = time.perf_counter()
         try:
             res = pending.result()
         finally:
+            self.wait_s += time.perf_counter() - t0
             self._inflight -= 1
-        return self._store(res)
+        self._store(res)
 
     def _take_jobs(self):
         """Snapshot the queues as engine-call arguments (main thread)."""
@@ -360,36 +388,64 @@ class BatchVerifier:
         fn = {"ct": "verify_ciphertexts", "sig": "verify_sig_shares", "dec": "verify_dec_shares"}
         return [(kind, keys, getattr(self.eng, fn[kind])(*args)) for kind, keys, args in jobs]
 
-    def _store(self, results):
-        """Cache verdicts (main thread) and return them as {(kind, instance, item): verdict}.
-        Verdicts of instances whose last running instance terminated while the drain was in
-        flight are not cached, so a terminated instance leaves nothing behind."""
-        fresh = {}
+    def _store(self, results, want=None):
+        """Cache verdicts (main thread).  Verdicts of instances whose last running instance
+        terminated while the drain was in flight are not cached, so a terminated instance leaves
+        nothing behind.  want = (kind, instance key, item key): that verdict is returned (a
+        synchronous *_valid reads its verdict from here even when no running instance keeps it)."""
         rel = self._released
+        got = None
         for kind, keys, v in results:
             self._count(len(keys))
-            if kind == "ct":
+            if kind == "sig":
+                cache = self._sig
                 for k, ok in zip(keys, v):
-                    c = (k[2], k[1])
-                    fresh[("ct", c, k[0])] = bool(ok)
-                    if c not in rel:
-                        self._ct.setdefault(c, {})[k[0]] = bool(ok)
-            elif kind == "sig":
-                for k, ok in zip(keys, v):
-                    fresh[("sig", k[1], (k[0], k[2]))] = bool(ok)
-                    if k[1] not in rel:
-                        self._sig.setdefault(k[1], {})[(k[0], k[2])] = bool(ok)
-            else:
+                    h = k[1]
+                    d = cache.get(h)
+                    if d is None:  # an existing entry is never a released instance's (release pops it)
+                        if h in rel:
+                            continue
+                        d = cache[h] = {}
+                    d[(k[0], k[2])] = ok == 1
+            elif kind == "dec":
+                cache = self._dec
                 for k, ok in zip(keys, v):
                     c = (k[2], k[3])
-                    fresh[("dec", c, (k[0], k[1]))] = bool(ok)
-                    if c not in rel:
-                        self._dec.setdefault(c, {})[(k[0], k[1])] = bool(ok)
+                    d = cache.get(c)
+                    if d is None:
+                        if c in rel:
+                            continue
+                        d = cache[c] = {}
+                    d[(k[0], k[1])] = ok == 1
+            else:
+                cache = self._ct
+                for k, ok in zip(keys, v):
+                    c = (k[2], k[1])
+                    d = cache.get(c)
+                    if d is None:
+                        if c in rel:
+                            continue
+                        d = cache[c] = {}
+                    d[k[0]] = ok == 1
+            if want is not None and want[0] == kind:
+                for k, ok in zip(keys, v):
+                    if self._item(kind, k) == want[1:]:
+                        got = ok == 1
+                        break
         # nothing queued after the last release can name the released instance (the drivers
         # queue only for running instances), so the set only has to outlive the drains in flight
         if not self._inflight:
             self._released.clear()
-        return fresh
+        return got
+
+    @staticmethod
+    def _item(kind, k):
+        """(instance key, item key) of a queued check."""
+        if kind == "sig":
+            return k[1], (k[0], k[2])
+        if kind == "dec":
+            return (k[2], k[3]), (k[0], k[1])
+        return (k[2], k[1]), k[0]
 
     def _count(self, n):
         self.calls += 1

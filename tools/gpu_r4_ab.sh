@@ -20,13 +20,18 @@ for r in $(seq ${REPS:-2}); do
     done
   done
 done
-if [ -n "$PROF" ]; then
+for PL in $PROF; do
+  [ "$PL" = "1" ] || [ "$PL" = "intree" ] && export -n HBBFT_HIP_LIB || export HBBFT_HIP_LIB=$R/hbbft_amd/ab/$PL.so
   cd /tmp
   B="$R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-combine --streams 1 --workload ${PROF_W:-sign}"
-  mkdir -p $O/prof
-  timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof/trace -o run -- python3 $B > $O/prof/trace.log 2>&1 || { echo "trace failed"; tail -5 $O/prof/trace.log; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d $O/prof/sq -o run -- python3 $B > $O/prof/sq.log 2>&1 || { echo "sq failed"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/prof/fetch -o run -- python3 $B > $O/prof/fetch.log 2>&1 || { echo "fetch failed"; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof/write -o run -- python3 $B > $O/prof/write.log 2>&1 || { echo "write failed"; exit 1; }
-fi
+  P=$O/prof_$PL
+  mkdir -p $P
+  timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run -- python3 $B > $P/trace.log 2>&1 || { echo "trace failed"; tail -5 $P/trace.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --output-format csv -d $P/sq -o run -- python3 $B > $P/sq.log 2>&1 || { echo "sq failed"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE --output-format csv -d $P/icache -o run -- python3 $B > $P/icache.log 2>&1 || { echo "icache failed"; tail -3 $P/icache.log; }
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/fetch -o run -- python3 $B > $P/fetch.log 2>&1 || { echo "fetch failed"; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -o run -- python3 $B > $P/write.log 2>&1 || { echo "write failed"; exit 1; }
+  cd $R
+done
+unset HBBFT_HIP_LIB
 echo done

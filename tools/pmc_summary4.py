@@ -28,6 +28,9 @@ for k in sorted(set(agg) | set(dur)):
             100 * c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"], 100 * c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"])
     if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
         line += " | HBM %.2f GB" % ((2 * c.get("FETCH_SIZE", 0) + c.get("WRITE_SIZE", 0)) * 1024 / 1e9)
+    if c.get("SQC_ICACHE_REQ"):
+        line += " | icache hit %.1f%% (%.2fG req)" % (100 * c.get("SQC_ICACHE_HITS", 0) / c["SQC_ICACHE_REQ"],
+                                                    c["SQC_ICACHE_REQ"] / 1e9)
     if "SQ_INSTS_VMEM_RD" in c:
         line += " | vmem rd %.0f wr %.0f /wave" % (c["SQ_INSTS_VMEM_RD"] / max(c.get("SQ_WAVES", 1), 1),
                                                   c.get("SQ_INSTS_VMEM_WR", 0) / max(c.get("SQ_WAVES", 1), 1))

@@ -53,7 +53,7 @@ for d in sys.argv[2:]:
         fb = fetch[k].get("FETCH_SIZE", 0.0) * 1024 * 2
         wb = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
         e = {"fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
-             "avg_ns": dur.get(k), "source": os.path.basename(os.path.normpath(d))}
+             "avg_ns": dur.get(k), "source": os.path.basename(os.path.normpath(d)).replace("pmc_", "", 1)}
         if k in sq:
             e["sq"] = sq[k]
             w = sq[k].get("SQ_WAVE_CYCLES")
