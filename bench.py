@@ -44,11 +44,12 @@ ACK_LANE_MIN = 65536                            # HBH_ACK_LANE_MIN (include/hbbf
 MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
-IMPLS = {"auto": 3, "pair": 4, "wave": 5}   # HBH_IMPL_* (include/hbbft_hip.h)
+IMPLS = {"auto": 3, "pair": 4, "wave": 5, "quad": 6}   # HBH_IMPL_* (include/hbbft_hip.h)
 PAIR_SIGN = "hbs::k_pair_verify<false, true, 2>"
 PAIR_DECRYPT = "hbs::k_pair_verify<false, false, 0>"
 KERNEL_NAMES = {"pair": PAIR_SIGN,
                 "wave": "hbs::k_wave (one wave per check)",
+                "quad": "hbs::k_quad_verify<false, true, 2>",
                 "auto": PAIR_SIGN,
                 "decrypt": PAIR_DECRYPT}
 G1_UNC = bytes.fromhex(
@@ -258,9 +259,10 @@ def reference_work(main_k, workcount):
                     "final exp)); the kernel's own count is roofline.mad_per_unit"}
 
 
-def pair_waves_per_simd(checks):
-    """The lane-pair kernel k_pair_verify: two lanes per check, 64-lane waves, 1,024 SIMDs."""
-    w = checks * 2 / 64 / 1024
+def pair_waves_per_simd(checks, lanes=2):
+    """Waves per SIMD of the lane-pair kernel k_pair_verify (two lanes per check) or the lane-quad
+    kernel k_quad_verify (lanes=4): 64-lane waves, 1,024 SIMDs."""
+    w = checks * lanes / 64 / 1024
     return 2 if w >= 2 else (1 if w >= 1 else round(w, 3))
 
 
@@ -435,7 +437,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
-    ap.add_argument("--impl", choices=["pair", "wave", "auto"], default="auto",
+    ap.add_argument("--impl", choices=["pair", "wave", "quad", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
@@ -542,10 +544,11 @@ def main():
     if rank == 0:
         kern_ms = pair_ms / max(pair_n, 1)
         main_k = roofline_entry(KERNEL_NAMES[args.impl], pair_n, kern_ms, n, workcount.PAIR_CHECK_WALK, "share check",
-                                pair_waves_per_simd(n) if args.impl in ("pair", "auto") else None)
+                                pair_waves_per_simd(n, 4 if args.impl == "quad" else 2)
+                                if args.impl in ("pair", "auto", "quad") else None)
         kernels = [main_k]
         if prep_n:
-            kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto") else "hb::k_g2_prepare",
+            kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto", "quad") else "hb::k_g2_prepare",
                                           prep_n, prep_ms / prep_n, nh, workcount.PAIR_PREP_DOC, "document (G2 walk)",
                                           nh * 2 / 64 / 1024))
         out = {
@@ -1031,7 +1034,10 @@ def run_epoch_bench(args, eng, world, rank, dev):
                     "host_ms": phases["epoch"] - sum(waits.values()), "gpu_kernel_ms": sum(kern.values()),
                     "blocked_by_phase_ms": waits, "gpu_kernel_by_stage_ms": kern}
         host_gpu["host_over_gpu"] = host_gpu["host_ms"] / max(host_gpu["gpu_kernel_ms"], 1e-9)
-        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX checks (all of an epoch's) to the wave kernel.
+        if args.pipeline:
+            host_gpu["pipelined_ms"] = {k: sum(r.overlap.get(k, 0.0) for r in results) / len(results) * 1e3
+                                        for k in ("hand_s", "worker_engine_s")}
+        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (5,120) checks -- the epoch's -- to the wave kernel.
         main_k = roofline_entry("hbs::k_wave", pair_n, pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
                                 workcount.PAIR_CHECK_WALK, "share / ciphertext check")
         line = {

@@ -155,7 +155,7 @@ int end_call(hbh_engine* e, hipStream_t s) {
 
 int resolve_impl(const hbh_engine* e, size_t n) {
   if (e->impl != HBH_IMPL_AUTO) return e->impl;
-  return n <= HBH_AUTO_WAVE_MAX ? HBH_IMPL_WAVE : HBH_IMPL_PAIR;
+  return n <= HBH_AUTO_WAVE_MAX ? HBH_IMPL_WAVE : (n <= HBH_AUTO_QUAD_MAX ? HBH_IMPL_QUAD : HBH_IMPL_PAIR);
 }
 
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
@@ -180,6 +180,8 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
   if (impl == HBH_IMPL_WAVE)
     HBH_CHECK(hbl::wave_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  else if (impl == HBH_IMPL_QUAD)
+    HBH_CHECK(hbl::quad_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   else
     HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   e->timer.end(s, t);
@@ -419,7 +421,7 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
-  if (impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO && impl != HBH_IMPL_WAVE)
+  if (impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO && impl != HBH_IMPL_WAVE && impl != HBH_IMPL_QUAD)
     return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;

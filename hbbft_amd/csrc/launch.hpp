@@ -1,5 +1,5 @@
 // Host-side launchers of the HIP kernels.  Each kernel family lives in its own translation unit
-// (k_pair.hip, k_wave.hip, k_curve.hip, k_g1quad.hip, k_interp_pair.hip, k_wire.hip) so the Makefile
+// (k_pair.hip, k_quad.hip, k_wave.hip, k_curve.hip, k_g1quad.hip, k_interp_pair.hip, k_wire.hip) so the Makefile
 // compiles them in parallel; engine.hip owns the C ABI, device buffers and streams and calls only
 // these functions.
 #pragma once
@@ -29,6 +29,13 @@ hipError_t pair_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* 
 // flags: bit 0 negates P2 (pairing equality), bit 1 conjugates f (single pairing value, with
 // value_out: e(P1,Q1)^3 e(P2,Q2)^3 as 144 canonical words per check)
 hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
+                       uint8_t* verdict, uint32_t* value_out);
+
+// --------------------------------------------------------------- lane-quad pairing (k_quad.hip)
+// The same verdicts / values as pair_verify with FOUR lanes per check (two lane pairs splitting
+// each step's independent products): the mid-size batches, one wave per SIMD at 16,384 checks.
+// TABLE sides read pair_prep tables.
+hipError_t quad_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
                        uint8_t* verdict, uint32_t* value_out);
 
 // --------------------------------------------------------------- wave-per-check pairing (k_wave.hip)

@@ -281,6 +281,7 @@ class EpochResult:
         self.checks_consumed = 0  # verdicts the flows used (the reference's per-message checks)
         self.combines = 0
         self.wait = {}          # phase -> seconds the flows spent blocked on engine calls
+        self.overlap = {}       # pipelined drains: host handling beside a drain in flight, worker engine time
         self.ba_decisions = {}  # proposer -> BA decision (BA-driven coins)
         self.ba_coins = {}      # proposer -> {BA epoch: threshold coin}
         self.ba_queued = 0      # coin shares that waited in a BA future-epoch queue
@@ -338,7 +339,10 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
             continue
         pending = verifier.drain_async()
         if prev is not None:
+            t0 = time.perf_counter()
             yield from hand(prev)
+            if res is not None:
+                res.overlap["hand_s"] = res.overlap.get("hand_s", 0.0) + time.perf_counter() - t0
         verifier.commit(pending)
         prev = batch
     if prev is not None:
@@ -578,7 +582,9 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
             continue
         pending = ver.drain_async()
         if prev is not None:
+            t0 = time.perf_counter()
             hand_window(*prev)
+            res.overlap["hand_s"] = res.overlap.get("hand_s", 0.0) + time.perf_counter() - t0
         ver.commit(pending)
         prev = (batch, w0 + len(batch))
     if prev is not None:
@@ -727,6 +733,8 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
     res.timing["output"] = time.perf_counter() - t0
     res.timing["epoch"] = time.perf_counter() - t_all
     res.engine_calls, res.checks_gpu, res.checks_consumed = ver.calls, ver.checks, ver.lookups
+    if pipelined:
+        res.overlap["worker_engine_s"] = ver.async_s
     res.combines = len(coin_out) + len(dec_out)
     return res
 

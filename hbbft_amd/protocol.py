@@ -149,6 +149,7 @@ class BatchVerifier:
         self._open = {}         # instance key -> number of running instances that use it
         self._inflight = 0      # drain_async calls not yet committed
         self.wait_s = 0.0       # time the calling thread spent blocked on engine calls (drains, combines)
+        self.async_s = 0.0      # drain_async: time of the engine calls on the worker thread
 
     # -------------------------------------------------------------- host hashing
     def hash_docs(self, docs):
@@ -349,7 +350,14 @@ class BatchVerifier:
         self._inflight += 1
         if _POOL is None:
             _POOL = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="hbh-drain")
-        return _POOL.submit(self._run_jobs, jobs)
+        return _POOL.submit(self._run_jobs_timed, jobs)
+
+    def _run_jobs_timed(self, jobs):
+        t0 = time.perf_counter()
+        try:
+            return self._run_jobs(jobs)
+        finally:
+            self.async_s += time.perf_counter() - t0
 
     def commit(self, pending):
         """Wait for a ``drain_async`` and cache its verdicts."""

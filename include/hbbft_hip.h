@@ -302,9 +302,14 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
  *     Throughput path.
  *   HBH_IMPL_WAVE (k_wave.hip): one 64-lane wave per check; the check's Fp2 products run on 32 lane
  *     pairs side by side.  Latency path (one check: the master check of combine_and_verify_sig).
- *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, PAIR above (the
- *     measured crossover with the CYC-run final exponentiation, profiles/r03/crossover_wave_pair_cyc.txt:
- *     8,192 checks 10.3 vs 12.4 ms, 12,288 checks 15.2 vs 12.5 ms; WAVE grows 1.24 ms per 1,024 checks).
+ *   HBH_IMPL_QUAD (k_quad.hip): FOUR lanes per check -- two lane pairs holding the check's state
+ *     side by side and splitting each step's independent products (k_pair's work per check in
+ *     ~0.55 of its per-lane time).  Mid-size path: 16,384 checks are one wave per SIMD.
+ *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, QUAD up to
+ *     HBH_AUTO_QUAD_MAX (one wave per SIMD), PAIR above -- the measured crossovers
+ *     (profiles/r04/c8_sweep_wave_quad_pair.txt, kernel ms per call on the sign workload): 4,096
+ *     checks WAVE 5.3 / QUAD 7.0 / PAIR 10.6; 8,192: 10.2 / 7.0 / 10.7; 16,384: 20.1 / 7.1 / 11.1;
+ *     24,576: QUAD 14.3 (two rounds of waves) / PAIR 11.2.
  * Retired (selecting them returns HBH_ERR_ARG): HBH_IMPL_THREAD (0, round 1's one-thread kernel),
  * HBH_IMPL_LANE_COOP (1, six lanes per check) and HBH_IMPL_THREAD_SIGNED (2, one thread per check
  * on signed limbs) -- WAVE and PAIR cover every batch size faster. */
@@ -314,7 +319,9 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_AUTO 3
 #define HBH_IMPL_PAIR 4
 #define HBH_IMPL_WAVE 5
-#define HBH_AUTO_WAVE_MAX 9728
+#define HBH_IMPL_QUAD 6
+#define HBH_AUTO_WAVE_MAX 5120
+#define HBH_AUTO_QUAD_MAX 16384
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 /* Ack-check kernel of hbh_bivar_ack_check_set: HBH_ACK_QUAD (k_bivar_check_quad: four lanes per ack
  * split each G1 operation, Jacobian rows -- latency), HBH_ACK_LANE (k_bivar_check: one lane per ack,

@@ -17,7 +17,7 @@ import pytest
 
 from oracle import bls12_381 as C
 from oracle import cbls, tc
-from hbbft_amd._lib import IMPL_AUTO, IMPL_WAVE
+from hbbft_amd._lib import IMPL_AUTO, IMPL_QUAD, IMPL_WAVE
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
 
 pytestmark = pytest.mark.gpu
@@ -54,7 +54,7 @@ def sign_batch(engine):
     return dict(coeffs=coeffs, sks=sks, pks=pks, mpk=mpk, hashes=hashes, sigs=sigs, expected=expected)
 
 
-@pytest.mark.parametrize("impl", [IMPL_AUTO, IMPL_WAVE], ids=["auto", "wave"])
+@pytest.mark.parametrize("impl", [IMPL_AUTO, IMPL_WAVE, IMPL_QUAD], ids=["auto", "wave", "quad"])
 def test_config1_65536_sig_shares(engine, sign_batch, impl):
     b = sign_batch
     n = NDOCS * N
@@ -71,13 +71,15 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
         assert cbls.verify_g2(b["pks"][i % N], b["sigs"][i], b["hashes"][i // N]) == bool(v[i]), i
 
 
-def test_config1_wave_at_auto_threshold(engine, sign_batch):
-    """Both kernels at the AUTO boundary (HBH_AUTO_WAVE_MAX = 9,728 checks: 152 documents of
-    configs[1]): WAVE walks both G2 sides, PAIR reads H's line table; verdicts equal the construction."""
+@pytest.mark.parametrize("n", [5120, 5184, 16384, 16448], ids=["wave_max", "quad_min", "quad_max", "pair_min"])
+def test_config1_at_auto_thresholds(engine, sign_batch, n):
+    """Every kernel on both sides of the AUTO boundaries (HBH_AUTO_WAVE_MAX = 5,120 checks, 80
+    documents of configs[1]; HBH_AUTO_QUAD_MAX = 16,384, 256 documents; one more document past
+    each): WAVE walks both G2 sides, QUAD and PAIR read H's line table; verdicts equal the
+    construction."""
     b = sign_batch
-    n = 9728
-    from hbbft_amd._lib import IMPL_PAIR
-    for impl in (IMPL_WAVE, IMPL_PAIR, IMPL_AUTO):
+    from hbbft_amd._lib import IMPL_PAIR, IMPL_QUAD
+    for impl in (IMPL_WAVE, IMPL_QUAD, IMPL_PAIR, IMPL_AUTO):
         engine.set_pairing_impl(impl)
         try:
             v = engine.verify_sig_shares([b["pks"][i % N] for i in range(n)], b["sigs"][:n], b["hashes"][:n // N],

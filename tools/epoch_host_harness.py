@@ -38,10 +38,18 @@ class HostEngine:
         return hoststage.g2_mul(list(pts), list(scalars), threads=self.threads)
 
     # verdicts
+    sleep_base, sleep_per = 0.0, 0.0  # emulated device time per call (time.sleep releases the GIL)
+
+    def _device(self, n):
+        if self.sleep_base or self.sleep_per:
+            time.sleep(self.sleep_base + n * self.sleep_per)
+
     def verify_sig_shares(self, pks, sigs, hashes, doc_idx):
+        self._device(len(pks))
         return bytes(1 if (bytes(p), bytes(s)) in self.valid else 0 for p, s in zip(pks, sigs))
 
     def verify_dec_shares(self, shares, pks, huv, w, ct_idx):
+        self._device(len(pks))
         return bytes(1 if (bytes(p), bytes(s)) in self.valid else 0 for s, p in zip(shares, pks))
 
     def verify_ciphertexts(self, us, ws, huv):
@@ -90,8 +98,12 @@ def main():
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--prefetch", action="store_true", help="coin documents prefetched (here: same epoch)")
+    ap.add_argument("--pipeline", action="store_true")
+    ap.add_argument("--device-ms", default="0,0", help="emulated device time per drain: base ms, ms per check")
     args = ap.parse_args()
     eng = HostEngine()
+    b, per = (float(x) for x in args.device_ms.split(","))
+    eng.sleep_base, eng.sleep_per = b / 1e3, per / 1e3
     cache = os.path.join("/tmp", "epoch_host_trace.pkl")
     if os.path.exists(cache):
         with open(cache, "rb") as f:
@@ -111,7 +123,7 @@ def main():
         if pr:
             pr.enable()
         pf = prefetch_coins(keys, tr.hb_epoch, range(keys.n)) if args.prefetch else None
-        res = run_epoch(eng, keys, tr, window=4096, coin_prefetch=pf)
+        res = run_epoch(eng, keys, tr, window=4096, coin_prefetch=pf, pipelined=args.pipeline)
         if pr:
             pr.disable()
         ms = (time.perf_counter() - t0) * 1e3

@@ -20,7 +20,16 @@ def disasm(path):
         elf = os.path.join(d, "dev.elf")
         r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={path}",
                             "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={elf}"], capture_output=True)
-        src = elf if r.returncode == 0 and os.path.getsize(elf) > 0 else path
+        if r.returncode != 0 or not os.path.exists(elf) or os.path.getsize(elf) == 0:
+            # new-driver objects and shared libraries keep the bundle in the .hip_fatbin section
+            fb = os.path.join(d, "fatbin")
+            subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", path, os.path.join(d, "x")],
+                           capture_output=True)
+            if os.path.exists(fb):
+                r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={elf}"],
+                                   capture_output=True)
+        src = elf if r.returncode == 0 and os.path.exists(elf) and os.path.getsize(elf) > 0 else path
         out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", src], capture_output=True, text=True)
         return out.stdout.split("\n")
 
