@@ -995,6 +995,11 @@ def run_epoch_bench(args, eng, world, rank, dev):
         dist.barrier()
     results = []
     eng.set_profiling(True)
+    ceng = None
+    if args.pipeline:  # pipelined combines run on a second engine: its kernels count as GPU time too
+        from hbbft_amd.honey_badger import combine_engine
+        ceng = combine_engine(eng)
+        ceng.set_profiling(True)
     prof = None
     if args.profile_epoch:
         import cProfile
@@ -1014,9 +1019,11 @@ def run_epoch_bench(args, eng, world, rank, dev):
         with open(args.profile_epoch, "w") as fh:
             pstats.Stats(prof, stream=fh).sort_stats("tottime").print_stats(45)
     pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
-    stage_ms = {name: eng.stage_time(st)[0] for name, st in
+    stage_ms = {name: eng.stage_time(st)[0] + (ceng.stage_time(st)[0] if ceng else 0.0) for name, st in
                 (("line_tables", STAGE_PREPARE), ("pairing", STAGE_PAIRING), ("curve", STAGE_CURVE))}
     eng.set_profiling(False)
+    if ceng:
+        ceng.set_profiling(False)
     for tr, r in zip(traces[args.warmup:-1], results):
         ok = ok and r.plaintexts == tr.proposals and len(r.coins) == len(tr.coin_docs)
         if args.epoch_coins == "ba":

@@ -1511,9 +1511,12 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, bool affine, size_t n, const uin
 
 // Acks in order of y (stable): the lanes of a wave then run the same small-scalar double-and-add.
 // y is a node index + 1, so a counting sort does it in O(n) (10^6 acks of a network-wide check).
-// (Round 4 measured tiles of 64 row slots ordered by y inside a tile, each XCD on a contiguous range
-// of workgroups, to keep a wave's rows in L2: 10^6 acks 57.5-58.2 ms against 53.7-54.2 ms for this
-// order on the same box, profiles/r04/c3_ab.txt -- kept as is.)
+// Round 4 measured (row tile, y) orders, whose waves re-read one tile's rows while they sit in L2:
+// HBM traffic per 10^6 acks falls from 4.68 GB (this order) to 0.74 GB (tiles of 256 row slots) and
+// 0.24 GB (1,024), but the launch is SLOWER at every tile size -- 54.2 ms here, 57.5 (64), 61.8-62.2
+// (256), 60.6-60.8 (1,024), 57.4 (4,096) (profiles/r04/c11_ack_tile_traffic.txt; with an XCD-
+// contiguous workgroup map as well: 57.5-58.2 ms, c3_ab.txt).  The kernel is VALU-bound at two
+// waves per SIMD (255 VGPRs) and its row fetches overlap the Horner arithmetic, so this order stays.
 void order_by_y(size_t n, const uint32_t* ys, std::vector<uint32_t>& order) {
   order.resize(n);
   uint32_t ymax = 0;

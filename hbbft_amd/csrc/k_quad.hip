@@ -16,6 +16,11 @@
 #include "launch.hpp"
 #include "pair_side.hpp"
 
+// waves per SIMD the kernel is compiled for (1: up to 512 registers per lane; 2: 256, A/B builds)
+#ifndef HBS_QUAD_WAVES
+#define HBS_QUAD_WAVES 1
+#endif
+
 namespace hbs {
 
 template <bool PLUS1>
@@ -50,7 +55,7 @@ HP_D H12 q_final_exp(const H12& f, uint32_t* __restrict__ stash) {
 
 // GEN: 0 = both P read per check, 1 = P1 is the generator, 2 = P2 is the generator
 template <bool W1, bool W2, int GEN>
-__global__ void __launch_bounds__(256, 1) k_quad_verify(PairArgs a) {
+__global__ void __launch_bounds__(256, HBS_QUAD_WAVES) k_quad_verify(PairArgs a) {
   extern __shared__ uint32_t stash_lds[];
   const int i = (int)((blockIdx.x * 256u + threadIdx.x) >> 2);
   if (i >= a.n) return;  // the four lanes of a quad leave together

@@ -391,6 +391,16 @@ def _decoder(engine, raw_msgs, out, fn):
 
 
 _HOST = None  # one worker for host-stage crypto that overlaps the flows (ctypes calls release the GIL)
+_COMBINE_ENGINES = {}  # id(engine) -> (engine, a second engine on its device for pipelined combines)
+
+
+def combine_engine(engine):
+    """The second engine (own stream and lock) that a pipelined epoch's combines run on, so a BA
+    window's coin combines proceed while the next window's drain holds the first engine."""
+    key = id(engine)
+    if key not in _COMBINE_ENGINES:
+        _COMBINE_ENGINES[key] = (engine, type(engine)(engine.device))
+    return _COMBINE_ENGINES[key][1]
 
 
 def _host_pool():
@@ -442,7 +452,7 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     # the background host work leaves two of the host threads to the flows and the drain worker
     bg = threads if threads else max(1, hoststage.host_threads() - 2)
     prep = None if raw else _host_pool().submit(_decrypt_prep, trace.cts, keys.sks[our], bg)
-    ver = BatchVerifier(engine)
+    ver = BatchVerifier(engine, combine_engine(engine) if pipelined and hasattr(engine, "device") else None)
     ver.recording = defer                  # combines of the epoch run in one batch at the end
     sk = keys.sks[our]
     n = keys.n

@@ -134,8 +134,11 @@ class BatchVerifier:
     queued check in one engine call per kind; ``*_valid`` returns a cached verdict (or verifies a
     single miss immediately).  ``calls`` counts engine calls (the batching evidence in tests)."""
 
-    def __init__(self, engine):
+    def __init__(self, engine, combine_engine=None):
         self.eng = engine
+        # combines on their own engine (stream) when given: a flow that combines while a
+        # drain_async is in flight then does not wait for the drain's engine call
+        self.ceng = combine_engine if combine_engine is not None else engine
         self._sig, self._dec, self._ct = {}, {}, {}
         self._qsig, self._qdec, self._qct = [], [], []
         self.calls = 0
@@ -188,7 +191,7 @@ class BatchVerifier:
             self._rec_g2.append(d)
             return d, 0, True
         t0 = time.perf_counter()
-        out, st, v = self.eng.combine_verify_g2(t, [list(idx)], [list(shares)], master_pk, [h])
+        out, st, v = self.ceng.combine_verify_g2(t, [list(idx)], [list(shares)], master_pk, [h])
         self.wait_s += time.perf_counter() - t0
         self.calls += 1
         return out[0], st[0], bool(v[0])
@@ -201,7 +204,7 @@ class BatchVerifier:
             self._rec_g1.append(d)
             return d, 0
         t0 = time.perf_counter()
-        out, st = self.eng.interpolate_g1(t, [list(idx)], [list(shares)])
+        out, st = self.ceng.interpolate_g1(t, [list(idx)], [list(shares)])
         self.wait_s += time.perf_counter() - t0
         self.calls += 1
         return out[0], st[0]
@@ -214,7 +217,7 @@ class BatchVerifier:
         for d in self._rec_g2:
             groups.setdefault((d.key[0], d.key[3]), []).append(d)
         for (t, mpk), ds in groups.items():
-            out, st, v = self.eng.combine_verify_g2(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds],
+            out, st, v = self.ceng.combine_verify_g2(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds],
                                                     mpk, [d.key[4] for d in ds])
             self.calls += 1
             for d, o, s_, vv in zip(ds, out, st, v):
@@ -223,7 +226,7 @@ class BatchVerifier:
         for d in self._rec_g1:
             groups.setdefault(d.key[0], []).append(d)
         for t, ds in groups.items():
-            out, st = self.eng.interpolate_g1(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds])
+            out, st = self.ceng.interpolate_g1(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds])
             self.calls += 1
             for d, o, s_ in zip(ds, out, st):
                 d.result = (o, s_)
