@@ -441,7 +441,9 @@ def main():
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
-    ap.add_argument("--window", type=int, default=4096, help="epoch workload: messages per verifier drain")
+    ap.add_argument("--window", type=int, default=8192,
+                    help="epoch workload: messages per verifier drain (8,192: 5 engine calls per epoch; 4,096: 9, "
+                         "15.1 vs 12.4 epochs/s, profiles/r04/c12_epoch_windows.txt)")
     ap.add_argument("--epoch-coins", choices=["ba", "synthetic"], default="ba",
                     help="epoch workload: coins from Binary Agreement instances or one ThresholdSign each")
     ap.add_argument("--ack-impl", choices=["auto", "quad", "lane"], default="auto",
@@ -550,7 +552,7 @@ def main():
         if prep_n:
             kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto", "quad") else "hb::k_g2_prepare",
                                           prep_n, prep_ms / prep_n, nh, workcount.PAIR_PREP_DOC, "document (G2 walk)",
-                                          nh * 2 / 64 / 1024))
+                                          nh * 4 / 64 / 1024))  # one lane quad per point
         out = {
             "metric": METRIC, "value": value, "unit": "shares/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
@@ -695,7 +697,7 @@ def run_decrypt(args, eng, world, rank, dev):
         if prep_n:
             kernels.append(roofline_entry("hbs::k_pair_prep", prep_n, prep_ms / prep_n, 2 * len(mine),
                                           workcount.PAIR_PREP_DOC, "G2 point (H_uv, W) walk",
-                                          2 * len(mine) * 2 / 64 / 1024))
+                                          2 * len(mine) * 4 / 64 / 1024))  # one lane quad per point
         line = {
             "metric": "verified decryption shares/sec (whole node), N=64 f=21", "value": total / (ms_step / 1e3),
             "unit": "shares/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
@@ -1070,7 +1072,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
                                   "verifies) run below one wave per SIMD: latency-bound; no single occupancy ceiling"),
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline_epoch(eng, keys, traces[-1], results[-1])
+            # the last timed epoch's trace (traces[-1] only feeds the last prefetch)
+            line["cpu_baseline"] = cpu_baseline_epoch(eng, keys, traces[args.warmup + len(results) - 1], results[-1])
         print(json.dumps(line), flush=True)
 
 
