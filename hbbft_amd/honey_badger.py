@@ -310,7 +310,8 @@ def _deliver(verifier, msgs, window, instance, queue, handle, res, kind, pipelin
             except ProtocolError as e:  # the reference's Err from handle_message (immediate combines)
                 res.errors.append((kind, p, e))
                 continue
-            res.faults += [(kind, p, f) for f in step.fault_log]
+            if step.fault_log:
+                res.faults += [(kind, p, f) for f in step.fault_log]
             if step.output:
                 yield p, step.output[0]
 
@@ -514,9 +515,10 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
     queued_n = {}
 
     def record(p, step):
-        res.faults += [("coin", p, f) for f in step.fault_log]
-        for d in step.output:
-            res.ba_decisions[p] = d
+        if step.fault_log:
+            res.faults += [("coin", p, f) for f in step.fault_log]
+        if step.output:
+            res.ba_decisions[p] = step.output[-1]
 
     def local_events(pos):
         progressed = True
@@ -635,8 +637,10 @@ def _coins(engine, keys, trace, ver, window, our, threads, pipelined, limit, res
     coin_sh = {} if raw else trace.coin_shares
     dec_sh = {} if raw else trace.dec_shares
 
+    handed_coin = {p: handed.setdefault(("coin", p), []) for p in ts}
+
     def hand_coin(p, j):
-        handed.setdefault(("coin", p), []).append(j)
+        handed_coin[p].append(j)
         inst = ts[p]
         if inst.terminated:
             return _EMPTY
@@ -695,8 +699,10 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
         if step.output:
             dec_out[p] = step.output[0]
 
+    handed_dec = {p: handed.setdefault(("dec", p), []) for p in td}
+
     def hand_dec(p, j):
-        handed.setdefault(("dec", p), []).append(j)
+        handed_dec[p].append(j)
         inst = td[p]
         if inst.terminated:  # handle_message of a terminated instance is an empty Step (:183-185)
             return _EMPTY

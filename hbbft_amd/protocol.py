@@ -281,9 +281,14 @@ class BatchVerifier:
     # entries are released in O(1).
     # ThresholdSign: PublicKeyShare::verify_g2(share, H)  (src/threshold_sign.rs:223)
     def queue_sig(self, pk, h, share):
-        h = bytes(h)
-        if (bytes(pk), bytes(share)) not in self._sig.get(h, ()):
-            self._qsig.append((bytes(pk), h, bytes(share)))
+        if type(h) is not bytes:
+            h = bytes(h)
+        if type(pk) is not bytes:
+            pk = bytes(pk)
+        if type(share) is not bytes:
+            share = bytes(share)
+        if (pk, share) not in self._sig.get(h, ()):
+            self._qsig.append((pk, h, share))
 
     def cached_sig(self, pk, h, share):
         """The cached verdict of a share check, or None (no engine call)."""
@@ -291,8 +296,11 @@ class BatchVerifier:
 
     def sig_valid(self, pk, h, share):
         self.lookups += 1
-        h, k = bytes(h), (bytes(pk), bytes(share))
-        v = self._sig.get(h, {}).get(k)
+        if type(h) is not bytes:
+            h = bytes(h)
+        k = (pk if type(pk) is bytes else bytes(pk), share if type(share) is bytes else bytes(share))
+        d = self._sig.get(h)
+        v = d.get(k) if d is not None else None
         if v is None:
             self._qsig.append((k[0], h, k[1]))
             v = self._drain(("sig", h, k))
@@ -300,14 +308,20 @@ class BatchVerifier:
 
     # ThresholdDecrypt: PublicKeyShare::verify_decryption_share(share, ct)  (src/threshold_decrypt.rs:227)
     def queue_dec(self, pk, share, huv, w):
-        c = (bytes(huv), bytes(w))
-        if (bytes(pk), bytes(share)) not in self._dec.get(c, ()):
-            self._qdec.append((bytes(pk), bytes(share)) + c)
+        if type(pk) is not bytes:
+            pk = bytes(pk)
+        if type(share) is not bytes:
+            share = bytes(share)
+        c = (huv if type(huv) is bytes else bytes(huv), w if type(w) is bytes else bytes(w))
+        if (pk, share) not in self._dec.get(c, ()):
+            self._qdec.append((pk, share) + c)
 
     def dec_valid(self, pk, share, huv, w):
         self.lookups += 1
-        c, k = (bytes(huv), bytes(w)), (bytes(pk), bytes(share))
-        v = self._dec.get(c, {}).get(k)
+        c = (huv if type(huv) is bytes else bytes(huv), w if type(w) is bytes else bytes(w))
+        k = (pk if type(pk) is bytes else bytes(pk), share if type(share) is bytes else bytes(share))
+        d = self._dec.get(c)
+        v = d.get(k) if d is not None else None
         if v is None:
             self._qdec.append(k + c)
             v = self._drain(("dec", c, k))

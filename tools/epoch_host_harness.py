@@ -123,7 +123,7 @@ def main():
         if pr:
             pr.enable()
         pf = prefetch_coins(keys, tr.hb_epoch, range(keys.n)) if args.prefetch else None
-        res = run_epoch(eng, keys, tr, window=4096, coin_prefetch=pf, pipelined=args.pipeline)
+        res = run_epoch(eng, keys, tr, window=8192, coin_prefetch=pf, pipelined=args.pipeline)
         if pr:
             pr.disable()
         ms = (time.perf_counter() - t0) * 1e3
