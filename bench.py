@@ -456,6 +456,8 @@ def main():
     ap.add_argument("--pipeline", action="store_true",
                     help="epoch workload: drain window k on a worker thread while the flows handle window k - 1 "
                          "(measured slower than serial drains on MI355X, profiles/r04/c6_epoch_ab.txt)")
+    ap.add_argument("--no-preverify", action="store_true",
+                    help="epoch workload: no decryption-share pre-verification beside the coin phase")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="epoch workload: no next-epoch coin prefetch (hash and sign every coin document in "
                          "its own epoch)")
@@ -990,18 +992,19 @@ def run_epoch_bench(args, eng, world, rank, dev):
     pf = prefetch(0)
     for k, tr in enumerate(traces[:args.warmup]):
         nxt = prefetch(k + 1)
-        r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf)
+        r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf,
+                      preverify=not args.no_preverify)
         pf = nxt
         ok = ok and r.plaintexts == tr.proposals
     if world > 1:
         dist.barrier()
     results = []
     eng.set_profiling(True)
-    ceng = None
-    if args.pipeline:  # pipelined combines run on a second engine: its kernels count as GPU time too
-        from hbbft_amd.honey_badger import combine_engine
-        ceng = combine_engine(eng)
-        ceng.set_profiling(True)
+    # the second engine (decryption-share pre-verification beside the coin phase; pipelined
+    # combines): its kernels count as GPU time too
+    from hbbft_amd.honey_badger import combine_engine
+    ceng = combine_engine(eng)
+    ceng.set_profiling(True)
     prof = None
     if args.profile_epoch:
         import cProfile
@@ -1010,7 +1013,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
     t0 = time.perf_counter()
     for k in range(args.warmup, len(traces) - 1):
         nxt = prefetch(k + 1)
-        results.append(run_epoch(eng, keys, traces[k], window=args.window, pipelined=args.pipeline, coin_prefetch=pf))
+        results.append(run_epoch(eng, keys, traces[k], window=args.window, pipelined=args.pipeline, coin_prefetch=pf,
+                                 preverify=not args.no_preverify))
         pf = nxt
     if pf is not None:
         pf.result()
@@ -1061,7 +1065,7 @@ def run_epoch_bench(args, eng, world, rank, dev):
                                       "queue, combines deferred per window)" if args.epoch_coins == "ba"
                                       else "synthetic: one ThresholdSign per BA instance at epoch 2"),
                        "pipelined_drains": args.pipeline,
-                       "coin_prefetch": pf_on,
+                       "coin_prefetch": pf_on, "dec_preverify": not args.no_preverify,
                        "parallelism": "one node per rank x%d" % world,
                        "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},
             "outputs_ok": ok, "phase_ms": phases, "host_vs_gpu": host_gpu,

@@ -1,4 +1,6 @@
 // HBH_IMPL_QUAD: the lane-quad pairing-equality kernel (gfx950) for mid-size batches.
+// (Kernel template; k_quad_g0/g1/g2.hip instantiate it per generator mode so the three ~3-minute
+// compiles run in parallel.)
 //
 // The same check as k_pair.hip -- FE(f_{|x|,Q1}(P1) f_{|x|,Q2}(-P2)) == 1, pairing 0.14's Miller loop
 // and final exponentiation -- on FOUR lanes per check: two lane pairs that hold the check's state
@@ -12,14 +14,9 @@
 // One wave per SIMD is the design point: __launch_bounds__(256, 1) gives a lane up to 512 registers
 // (256 VGPR + 256 AGPR), so the two pairs' operand sets of a dual product stay in registers.  The
 // final exponentiation parks one Fp12 per lane in LDS (72 KiB per 256-lane workgroup), as k_pair.
-#define HS_MULFN static __device__ __noinline__
+#pragma once
 #include "launch.hpp"
 #include "pair_side.hpp"
-
-// waves per SIMD the kernel is compiled for (1: up to 512 registers per lane; 2: 256, A/B builds)
-#ifndef HBS_QUAD_WAVES
-#define HBS_QUAD_WAVES 1
-#endif
 
 namespace hbs {
 
@@ -55,7 +52,9 @@ HP_D H12 q_final_exp(const H12& f, uint32_t* __restrict__ stash) {
 
 // GEN: 0 = both P read per check, 1 = P1 is the generator, 2 = P2 is the generator
 template <bool W1, bool W2, int GEN>
-__global__ void __launch_bounds__(256, HBS_QUAD_WAVES) k_quad_verify(PairArgs a) {
+// (two waves per SIMD -- 256 registers, 4,112 VGPR spills -- measured slower: 16,384 checks 9.29 vs
+// 7.09 ms, 32,768 checks 15.5 vs 14.2 ms, profiles/r04/c10_ab.txt)
+__global__ void __launch_bounds__(256, 1) k_quad_verify(PairArgs a) {
   extern __shared__ uint32_t stash_lds[];
   const int i = (int)((blockIdx.x * 256u + threadIdx.x) >> 2);
   if (i >= a.n) return;  // the four lanes of a quad leave together
@@ -103,11 +102,13 @@ __global__ void __launch_bounds__(256, HBS_QUAD_WAVES) k_quad_verify(PairArgs a)
 
 }  // namespace hbs
 
+
 namespace hbl {
 
-hipError_t quad_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
+// launch the four WALK / TABLE variants of one generator mode G
+template <int G>
+hipError_t quad_launch(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
                        uint8_t* verdict, uint32_t* value_out) {
-  if (n <= 0) return hipSuccess;
   hbs::PairArgs a;
   a.n = n;
   const PairSideDesc* d[2] = {&d1, &d2};
@@ -126,26 +127,23 @@ hipError_t quad_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairS
   const dim3 grid((unsigned)((4 * (size_t)n + 255) / 256)), block(256);
   const size_t lds = (size_t)hbs::STASH_WORDS * 256 * 4;
   const bool w1 = d1.lines == nullptr, w2 = d2.lines == nullptr;
-  const int gen = (d1.p == nullptr) == (d2.p == nullptr) ? 0 : (d1.p == nullptr ? 1 : 2);
-#define HBS_QUAD_LAUNCH(G)                                                                 \
-  do {                                                                                     \
-    if (w1 && w2)                                                                          \
-      hipLaunchKernelGGL((hbs::k_quad_verify<true, true, G>), grid, block, lds, s, a);     \
-    else if (w1)                                                                           \
-      hipLaunchKernelGGL((hbs::k_quad_verify<true, false, G>), grid, block, lds, s, a);    \
-    else if (w2)                                                                           \
-      hipLaunchKernelGGL((hbs::k_quad_verify<false, true, G>), grid, block, lds, s, a);    \
-    else                                                                                   \
-      hipLaunchKernelGGL((hbs::k_quad_verify<false, false, G>), grid, block, lds, s, a);   \
-  } while (0)
-  if (gen == 1)
-    HBS_QUAD_LAUNCH(1);
-  else if (gen == 2)
-    HBS_QUAD_LAUNCH(2);
+  if (w1 && w2)
+    hipLaunchKernelGGL((hbs::k_quad_verify<true, true, G>), grid, block, lds, s, a);
+  else if (w1)
+    hipLaunchKernelGGL((hbs::k_quad_verify<true, false, G>), grid, block, lds, s, a);
+  else if (w2)
+    hipLaunchKernelGGL((hbs::k_quad_verify<false, true, G>), grid, block, lds, s, a);
   else
-    HBS_QUAD_LAUNCH(0);
-#undef HBS_QUAD_LAUNCH
+    hipLaunchKernelGGL((hbs::k_quad_verify<false, false, G>), grid, block, lds, s, a);
   return hipGetLastError();
 }
+
+// one per translation unit (k_quad_g0/g1/g2.hip)
+hipError_t quad_verify_g0(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
+                          uint8_t* verdict, uint32_t* value_out);
+hipError_t quad_verify_g1(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
+                          uint8_t* verdict, uint32_t* value_out);
+hipError_t quad_verify_g2(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
+                          uint8_t* verdict, uint32_t* value_out);
 
 }  // namespace hbl

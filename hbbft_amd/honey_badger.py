@@ -351,7 +351,7 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
 
 
 def run_epoch(engine, keys, trace, window=8192, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
-              defer=True, raw=False, ba=None, coin_prefetch=None):
+              defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
     ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
@@ -363,6 +363,8 @@ def run_epoch(engine, keys, trace, window=8192, our=0, threads=0, pipelined=Fals
     ``raw``: the node receives bincode bytes (``trace.serialize()``): contributions are decoded in
     one batch (DeserializeCiphertext faults, epoch_state.rs:377-381) and every window of share
     messages in one batch before it is queued (hbbft_amd.wire).
+    ``preverify``: the contributions' ciphertext checks and the first t + 1 + slack decryption shares
+    of each are checked on a second engine while the coin phase runs (_dec_preverify).
     ``ba``: the coins come from Binary Agreement instances (``trace.with_ba``; default: when the
     trace has a BA side) -- hbbft_amd.binary_agreement's epochs, fixed coins and future-epoch queue,
     our SBV / Conf outcomes released along the message stream, coin combines deferred per window."""
@@ -372,7 +374,8 @@ def run_epoch(engine, keys, trace, window=8192, our=0, threads=0, pipelined=Fals
     if pipelined and switch_interval:
         sys.setswitchinterval(switch_interval)
     try:
-        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch)
+        return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch,
+                          preverify)
     finally:
         sys.setswitchinterval(old)
 
@@ -391,7 +394,7 @@ def _decoder(engine, raw_msgs, out, fn):
     return decode
 
 
-_HOST = None  # one worker for host-stage crypto that overlaps the flows (ctypes calls release the GIL)
+_HOST = None  # workers for host-stage crypto that overlaps the flows (ctypes calls release the GIL)
 _COMBINE_ENGINES = {}  # id(engine) -> (engine, a second engine on its device for pipelined combines)
 
 
@@ -407,7 +410,8 @@ def combine_engine(engine):
 def _host_pool():
     global _HOST
     if _HOST is None:
-        _HOST = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="hbh-host")
+        # two: an epoch's own decryption prep never waits behind the next epoch's coin prefetch
+        _HOST = concurrent.futures.ThreadPoolExecutor(max_workers=2, thread_name_prefix="hbh-host")
     return _HOST
 
 
@@ -447,7 +451,38 @@ def prefetch_coins(keys, hb_epoch, proposers, our=0, ba_epochs=(2,), hb_id=0, th
     return _host_pool().submit(job)
 
 
-def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None):
+_DEC_POOL = None  # one worker: speculative decryption-share pre-verification on the second engine
+
+
+def _dec_preverify(engine2, keys, trace, prep, limit):
+    """Ciphertext::verify of every contribution and PublicKeyShare::verify_decryption_share of the
+    first ``limit`` shares (in arrival order) of each, on the second engine (own stream) while the
+    coin phase runs: a node holds the RBC-delivered ciphertexts and the decryption shares that
+    arrive for them before the Subset output starts the ThresholdDecrypt instances (they wait in the
+    instance until set_ciphertext / remove_invalid_shares, threshold_decrypt.rs:138-147, 204-217).
+    Verdicts are pure, so checking them early changes no Step; the decrypt phase finds them in the
+    cache and queues only the rest.  Returns the engine results for BatchVerifier._store (main
+    thread)."""
+    huv_of, _ = prep.result()
+    pre = BatchVerifier(engine2)
+    for p in sorted(trace.cts):
+        if p in huv_of:
+            u, v, w = trace.cts[p]
+            pre.queue_ct(Ciphertext(u, v, w, huv_of[p]))
+    cnt = {}
+    for p, j in trace.dec_msgs:
+        if p not in huv_of:
+            continue
+        c = cnt.get(p, 0)
+        if limit is not None and c >= limit:
+            continue
+        cnt[p] = c + 1
+        pre.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], huv_of[p], trace.cts[p][2])
+    return pre._run_jobs(pre._take_jobs())
+
+
+def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None,
+               preverify=True):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     # the background host work leaves two of the host threads to the flows and the drain worker
@@ -455,6 +490,17 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     prep = None if raw else _host_pool().submit(_decrypt_prep, trace.cts, keys.sks[our], bg)
     ver = BatchVerifier(engine, combine_engine(engine) if pipelined and hasattr(engine, "device") else None)
     ver.recording = defer                  # combines of the epoch run in one batch at the end
+    pre_box = []  # the pre-verification future, once started
+
+    def start_preverify():
+        # after the coin phase's first drain: the checks then share the GPU with the flows' host work
+        # (handling that window), not with the drain itself
+        global _DEC_POOL
+        if pre_box or not preverify or prep is None or not hasattr(engine, "device"):
+            return
+        if _DEC_POOL is None:
+            _DEC_POOL = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="hbh-pre")
+        pre_box.append(_DEC_POOL.submit(_dec_preverify, combine_engine(engine), keys, trace, prep, limit))
     sk = keys.sks[our]
     n = keys.n
     t_all = time.perf_counter()
@@ -462,7 +508,8 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     # --- Binary Agreement coins: ThresholdSign per BA instance that reaches a coin epoch
     t0 = time.perf_counter()
     if ba:
-        coin_out = _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined, coin_prefetch)
+        coin_out = _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined, coin_prefetch,
+                             start_preverify)
         coin_sh, dec_sh = ({}, {}) if raw else (trace.coin_shares, trace.dec_shares)
         handed = {}
         ni_sign = None
@@ -472,11 +519,14 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     else:
         coin_out, handed, ni_sign, ts, coin_sh, dec_sh = _coins(engine, keys, trace, ver, window, our, threads,
                                                                pipelined, limit, res, raw, sk, n, t0)
+    start_preverify()  # (no-op when already started; the synthetic coin phase starts it here)
     return _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n,
-                               t_all, coin_out, handed, ni_sign, ts, coin_sh, dec_sh, prep)
+                               t_all, coin_out, handed, ni_sign, ts, coin_sh, dec_sh, prep,
+                               pre_box[0] if pre_box else None)
 
 
-def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined=False, coin_prefetch=None):
+def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined=False, coin_prefetch=None,
+              after_first_drain=None):
     """The BA-driven coin phase: one BinaryAgreementCoin per proposer with a coin (trace.ba).
     Messages (p, e, j) come in windows; before a window's drain, every share of a running or
     FUTURE epoch of its instance is queued (coin documents are hashed when first seen; a future
@@ -590,6 +640,8 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
         queue_window(batch)
         if not pipelined:
             ver.drain()
+            if after_first_drain is not None:
+                after_first_drain()
             hand_window(batch, w0 + len(batch))
             continue
         pending = ver.drain_async()
@@ -657,7 +709,7 @@ def _coins(engine, keys, trace, ver, window, our, threads, pipelined, limit, res
 
 
 def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipelined, limit, res, raw, sk, n, t_all,
-                        coin_out, handed, ni_sign, ts, coin_sh, dec_sh, prep=None):
+                        coin_out, handed, ni_sign, ts, coin_sh, dec_sh, prep=None, dec_pre=None):
     # --- Subset output: the N ciphertexts into ThresholdDecrypt
     t0 = time.perf_counter()
     ps = sorted(trace.cts)
@@ -678,6 +730,11 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
     by_u = {cts[p].u: own_dec[p] for p in ps}
     ni_dec = NetworkInfo(our, range(n), keys.t, keys.master_pk, keys.pks, decrypt_share=lambda U: by_u[bytes(U)])
     td = {p: ThresholdDecrypt(ni_dec, ver) for p in ps}
+    if dec_pre is not None:  # the verdicts checked beside the coin phase (_dec_preverify) into the cache
+        t1 = time.perf_counter()
+        pre = dec_pre.result()
+        ver.wait_s += time.perf_counter() - t1
+        ver._store(pre)
     for p in ps:
         ver.queue_ct(cts[p])  # (our own decryption share is not verified, threshold_decrypt.rs:167)
     ver.drain()

@@ -43,12 +43,19 @@ def test_epoch_small_and_window_equivalence(engine, n):
     trace = EpochTrace.generate(engine, keys, rng, hb_epoch=1, bad_every=5, proposal_bytes=100)
     big = run_epoch(engine, keys, trace, window=1 << 20)
     check(trace, big, keys)
-    one = run_epoch(engine, keys, trace, window=1, pipelined=False)
+    one = run_epoch(engine, keys, trace, window=1, pipelined=False, preverify=False)
     check(trace, one, keys)
     assert (one.plaintexts, one.coins, one.signatures) == (big.plaintexts, big.coins, big.signatures)
     assert [(k, p, f.node_id, f.kind) for k, p, f in one.faults] == [(k, p, f.node_id, f.kind) for k, p, f in big.faults]
     # per-message verification checks exactly what the flows consume; the big window batches
     assert one.checks_gpu == one.checks_consumed
+    # decryption shares pre-verified beside the coin phase: same steps, at most t + 1 + slack extra
+    # checks per instance, and the consumed checks are the per-message run's
+    pre = run_epoch(engine, keys, trace, window=1, pipelined=False, preverify=True)
+    check(trace, pre, keys)
+    assert (pre.plaintexts, pre.coins, pre.signatures) == (big.plaintexts, big.coins, big.signatures)
+    assert [(k, p, f.node_id, f.kind) for k, p, f in pre.faults] == [(k, p, f.node_id, f.kind) for k, p, f in big.faults]
+    assert pre.checks_consumed == one.checks_consumed and pre.checks_gpu >= one.checks_gpu
     assert big.engine_calls < one.engine_calls
     # pipelined small windows (drain k on the GPU while window k - 1 is handled): same steps
     for w in (1, 3):

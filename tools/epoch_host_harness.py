@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--prefetch", action="store_true", help="coin documents prefetched (here: same epoch)")
     ap.add_argument("--pipeline", action="store_true")
+    ap.add_argument("--no-preverify", action="store_true")
+    ap.add_argument("--window", type=int, default=8192)
     ap.add_argument("--device-ms", default="0,0", help="emulated device time per drain: base ms, ms per check")
     args = ap.parse_args()
     eng = HostEngine()
@@ -117,13 +119,18 @@ def main():
         with open(cache, "wb") as f:
             pickle.dump((keys.__dict__, tr), f)
     teach(eng, keys, tr)
+    # the second engine of decryption-share pre-verification / pipelined combines: the same stand-in
+    import hbbft_amd.honey_badger as hb
+    eng.device = 0
+    hb._COMBINE_ENGINES[id(eng)] = (eng, eng)
     for r in range(args.reps):
         pr = cProfile.Profile() if args.profile and r == args.reps - 1 else None
         t0 = time.perf_counter()
         if pr:
             pr.enable()
         pf = prefetch_coins(keys, tr.hb_epoch, range(keys.n)) if args.prefetch else None
-        res = run_epoch(eng, keys, tr, window=8192, coin_prefetch=pf, pipelined=args.pipeline)
+        res = run_epoch(eng, keys, tr, window=args.window, coin_prefetch=pf, pipelined=args.pipeline,
+                        preverify=not args.no_preverify)
         if pr:
             pr.disable()
         ms = (time.perf_counter() - t0) * 1e3
