@@ -616,14 +616,22 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                     queued_n[(p, e)] = c + 1
 
     def hand_window(batch, end):
-        for p, e, j in batch:
+        for m in batch:
+            p, e, j = m
             b = bas[p]
-            if b.decision is not None:  # a decided instance ignores every message (:245-248)
+            # a decided instance ignores every message (:245-248); an expired epoch's coin message and
+            # a share for a coin already decided or pending are empty Steps (:250-252, _handle_coin):
+            # skipped here without building them
+            be = b.epoch
+            if b.decision is not None or e < be or (e == be and (b.coin_decided or b.pending is not None)):
                 continue
             try:
-                record(p, b.handle_message(j, e, ba.shares[(p, e, j)]))
+                step = b.handle_message(j, e, ba.shares[m])
             except ProtocolError as err:
                 res.errors.append(("coin", p, err))
+                continue
+            if step.fault_log or step.output:
+                record(p, step)
         resolve()
         local_events(end)
         resolve()

@@ -526,12 +526,18 @@ class ThresholdSign:
     def handle_message(self, sender_id, share):  # :181-197
         if self.terminated:
             return Step()
-        idx = self.netinfo.node_index(sender_id)
+        ni = self.netinfo
+        idx = ni._index.get(sender_id)  # node_index
         if idx is None:
             raise ProtocolError("UnknownSender")
-        if not self.is_share_valid(sender_id, share):
-            return Step.fault(sender_id, "UnverifiedSignatureShareSender")
-        self.received_shares[sender_id] = (idx, bytes(share))
+        # is_share_valid (:216-225), inlined on this per-message path
+        if self.doc_hash is not None:
+            pk = ni.pk_shares.get(sender_id)
+            if pk is None or not self.verifier.sig_valid(pk, self.doc_hash, share):
+                return Step.fault(sender_id, "UnverifiedSignatureShareSender")
+        self.received_shares[sender_id] = (idx, share if type(share) is bytes else bytes(share))
+        if self.doc_hash is None or len(self.received_shares) <= ni.t:  # try_output's gate (:227-247)
+            return Step()
         return self.try_output()
 
     def remove_invalid_shares(self):  # :200-213 -- the natural batch point: one drain
@@ -642,15 +648,21 @@ class ThresholdDecrypt:
     def handle_message(self, sender_id, share):  # :182-201
         if self.terminated:
             return Step()
-        idx = self.netinfo.node_index(sender_id)
+        ni = self.netinfo
+        idx = ni._index.get(sender_id)  # node_index
         if idx is None:
             raise ProtocolError("UnknownSender")
-        if not self.is_share_valid(sender_id, share):
-            return Step.fault(sender_id, "UnverifiedDecryptionShareSender")
+        ct = self.ciphertext
+        if ct is not None:  # is_share_valid (:220-229), inlined on this per-message path
+            pk = ni.pk_shares.get(sender_id)
+            if pk is None or not self.verifier.dec_valid(pk, share, ct.huv, ct.w):
+                return Step.fault(sender_id, "UnverifiedDecryptionShareSender")
         dup = sender_id in self.shares
-        self.shares[sender_id] = (idx, bytes(share))
+        self.shares[sender_id] = (idx, share if type(share) is bytes else bytes(share))
         if dup:
             return Step.fault(sender_id, "MultipleDecryptionShares")
+        if len(self.shares) <= ni.t:  # try_output's gate (:232-252)
+            return Step()
         return self.try_output()
 
     def remove_invalid_shares(self):  # :204-217 -- one drain for every share received early
