@@ -130,3 +130,49 @@ def test_two_threshold_sign_instances_same_document():
     assert b.terminated and sb.output == [b"S" * 192]
     assert [f.kind for f in sb.fault_log] == ["UnverifiedSignatureShareSender"]
     assert ver.cached() == 0
+
+
+def test_verdict_store_groups_per_instance_and_serves_a_sync_miss():
+    """Round 4's verdict store: dec and ct checks land under their ciphertext key, sig checks under
+    their document; a synchronous miss drains once and returns its own verdict."""
+    eng = FakeEngine()
+    ver = BatchVerifier(eng)
+    huv, w = b"H" * 192, b"W" * 192
+    ver.queue_dec(b"pk1", b"\x02s", huv, w)
+    ver.queue_dec(b"pk2", b"\x03s", huv, w)
+    ver.drain()
+    assert ver._dec[(huv, w)] == {(b"pk1", b"\x02s"): True, (b"pk2", b"\x03s"): False}
+    assert ver.dec_valid(b"pk1", b"\x02s", huv, w) is True and len(eng.calls) == 1
+    assert ver.dec_valid(b"pk3", b"\x05s", huv, w) is False and len(eng.calls) == 2   # miss: one drain
+    assert ver.sig_valid(bytearray(b"pk"), bytearray(b"D" * 8), bytearray(b"\x04s")) is True  # non-bytes keys
+    assert ver._sig[b"D" * 8] == {(b"pk", b"\x04s"): True}
+    assert ver.lookups == 3 and ver.checks == 4
+
+
+def test_add_doc_hashes_feeds_the_hash_cache():
+    """Prefetched document hashes (honey_badger.prefetch_coins) are served without hashing."""
+    ver = BatchVerifier(FakeEngine())
+    ver.add_doc_hashes({b"doc": b"H" * 192})
+    assert ver.doc_hash_of(b"doc") == b"H" * 192
+    assert ver.hash_doc(b"doc") == b"H" * 192     # set_document takes it out of the cache
+    assert b"doc" not in ver._docs
+
+
+def test_engine_wait_is_accounted():
+    """wait_s counts the time the calling thread spent in engine calls (the epoch line's
+    host / GPU split), async_s the worker's."""
+    import time as _t
+
+    class Slow(FakeEngine):
+        def verify_sig_shares(self, *a):
+            _t.sleep(0.02)
+            return super().verify_sig_shares(*a)
+
+    ver = BatchVerifier(Slow())
+    _fill(ver, docs=1)
+    ver.drain()
+    assert ver.wait_s >= 0.015
+    _fill(ver, docs=2)
+    w0 = ver.wait_s
+    ver.commit(ver.drain_async())
+    assert ver.async_s >= 0.015 and ver.wait_s >= w0

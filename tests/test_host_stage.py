@@ -115,3 +115,19 @@ def test_bad_arguments(hs):
     from hbbft_amd._lib import HbhError
     with pytest.raises(HbhError):
         hs.g1_compress([b"\xff" * 96])  # coordinates >= p
+
+
+def test_prefetch_coins_equals_hash_and_sign(hs):
+    """honey_badger.prefetch_coins: the next epoch's BA coin documents (bincode((hb_id, epoch,
+    proposer), BA epoch)) hashed and signed on the host-stage thread equal hash_g2 and sk * H."""
+    from types import SimpleNamespace
+    from hbbft_amd.binary_agreement import coin_document
+    from hbbft_amd.honey_badger import prefetch_coins
+    keys = SimpleNamespace(sks=[1234567, 89], pks=None)
+    got = prefetch_coins(keys, 5, [0, 3], our=1, threads=2).result()
+    docs = [coin_document(0, 5, p, 2) for p in (0, 3)]
+    assert sorted(got) == sorted(docs)
+    hashes = hs.hash_g2(docs)
+    sigs = hs.g2_mul(hashes, [89, 89])
+    for d, h, s in zip(docs, hashes, sigs):
+        assert got[d] == (h, s)
