@@ -5,10 +5,11 @@
 // The same check as k_pair.hip -- FE(f_{|x|,Q1}(P1) f_{|x|,Q2}(-P2)) == 1, pairing 0.14's Miller loop
 // and final exponentiation -- on FOUR lanes per check: two lane pairs that hold the check's state
 // side by side and split each step's independent products between them (qfp.hpp).  The lane-pair
-// kernel's latency floor is one lane pair's whole check (~12.4 ms); below ~32,768 checks it cannot
+// kernel's latency floor is one lane pair's whole check (10.6 ms); below ~32,768 checks it cannot
 // fill the SIMDs, and the wave-per-check kernel's interpreter overhead caps it at ~0.8 M checks/s.
 // Here a batch of 16,384 checks is 1,024 waves, one per SIMD, and a check takes ~0.55 of the lane
-// pair's per-lane products: the protocol's natural batch points (BA replays, remove_invalid_shares:
+// pair's per-lane products (7.1 ms per batch of <= 16,384, profiles/r04/c8_sweep_wave_quad_pair.txt):
+// the protocol's natural batch points (BA replays, remove_invalid_shares:
 // src/binary_agreement/binary_agreement.rs:250-264, 507-519; src/threshold_decrypt.rs:204-217).
 //
 // One wave per SIMD is the design point: __launch_bounds__(256, 1) gives a lane up to 512 registers
