@@ -180,8 +180,10 @@ class BinaryAgreementCoin:
             # prefix (cached verdicts count; unknown ones are assumed valid) plus a small slack
             need, have, queued = self.netinfo.num_faulty() + 1 + REPLAY_SLACK, 0, False
             for sender, share in replay:
+                if have >= need:
+                    break
                 pk = self.netinfo.public_key_share(sender)
-                if pk is None or have >= need:
+                if pk is None:
                     continue
                 v = self.verifier.cached_sig(pk, self.ts.doc_hash, share)
                 if v is None:
@@ -194,4 +196,6 @@ class BinaryAgreementCoin:
             step.extend(self._handle_coin(sender, share))
             if self.decision is not None:
                 return step
+            if self.coin_decided or self.pending is not None:
+                break  # every later _handle_coin of this replay is an empty Step (:355-363)
         return step
