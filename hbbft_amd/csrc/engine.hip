@@ -158,6 +158,20 @@ int resolve_impl(const hbh_engine* e, size_t n) {
   return n <= HBH_AUTO_WAVE_MAX ? HBH_IMPL_WAVE : (n <= HBH_AUTO_QUAD_MAX ? HBH_IMPL_QUAD : HBH_IMPL_PAIR);
 }
 
+// the checks [off, n) of a side: per-check P and index map (or per-check Q when there is no map)
+// advance by off; tables and shared Q tables stay
+hbl::PairSideDesc offset_side(const hbl::PairSideDesc& d, size_t off) {
+  hbl::PairSideDesc o = d;
+  if (o.p) o.p = (const uint8_t*)o.p + off * HBH_G1_BYTES;
+  if (o.idx) {
+    o.idx += off;
+  } else {  // identity map: Q is per check (nq == n, check_idx)
+    o.q = (const uint8_t*)o.q + off * HBH_G2_BYTES;
+    o.nq -= off;
+  }
+  return o;
+}
+
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
 // table (k_pair_prep); every other side is walked inside the verify kernel.
 int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
@@ -178,12 +192,21 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
     sd[k].qinf = (const uint8_t*)inf[k]->p;
   }
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  if (impl == HBH_IMPL_WAVE)
+  if (impl == HBH_IMPL_WAVE) {
     HBH_CHECK(hbl::wave_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
-  else if (impl == HBH_IMPL_QUAD)
+  } else if (impl == HBH_IMPL_QUAD) {
     HBH_CHECK(hbl::quad_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
-  else
+  } else if (e->impl == HBH_IMPL_AUTO && n > HBH_AUTO_SPLIT_LO && n <= HBH_AUTO_SPLIT_HI) {
+    // one lane-pair wave per SIMD for the first HBH_AUTO_SPLIT_LO checks, the rest (<= 16,384) on
+    // the lane-quad kernel after it: 11.5 + 7.1 ms instead of the lane pair's two-wave 20.5 ms
+    const size_t n1 = HBH_AUTO_SPLIT_LO;
+    HBH_CHECK(hbl::pair_verify(s, (int)n1, sd[0], sd[1], flags, d_v, d_value));
+    const hbl::PairSideDesc r0 = offset_side(sd[0], n1), r1 = offset_side(sd[1], n1);
+    HBH_CHECK(hbl::quad_verify(s, (int)(n - n1), r0, r1, flags, d_v ? d_v + n1 : nullptr,
+                               d_value ? d_value + n1 * 144 : nullptr));
+  } else {
     HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  }
   e->timer.end(s, t);
   return HBH_OK;
 }

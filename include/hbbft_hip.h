@@ -309,7 +309,9 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
  *     HBH_AUTO_QUAD_MAX (one wave per SIMD), PAIR above -- the measured crossovers
  *     (profiles/r04/c8_sweep_wave_quad_pair.txt, kernel ms per call on the sign workload): 4,096
  *     checks WAVE 5.3 / QUAD 7.0 / PAIR 10.6; 8,192: 10.2 / 7.0 / 10.7; 16,384: 20.1 / 7.1 / 11.1;
- *     24,576: QUAD 14.3 (two rounds of waves) / PAIR 11.2.
+ *     24,576: QUAD 14.3 (two rounds of waves) / PAIR 11.2.  Between 32,768 and 49,152 checks the lane
+ *     pair needs a second wave on some SIMDs (40,960: 20.5 ms), so AUTO runs the first 32,768 on
+ *     PAIR (one wave per SIMD, 11.5 ms) and the rest on QUAD (7.1 ms) on the same stream.
  * Retired (selecting them returns HBH_ERR_ARG): HBH_IMPL_THREAD (0, round 1's one-thread kernel),
  * HBH_IMPL_LANE_COOP (1, six lanes per check) and HBH_IMPL_THREAD_SIGNED (2, one thread per check
  * on signed limbs) -- WAVE and PAIR cover every batch size faster. */
@@ -322,6 +324,8 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_QUAD 6
 #define HBH_AUTO_WAVE_MAX 5120
 #define HBH_AUTO_QUAD_MAX 16384
+#define HBH_AUTO_SPLIT_LO 32768  /* AUTO: (32,768, 49,152] checks = PAIR on 32,768 + QUAD on the rest */
+#define HBH_AUTO_SPLIT_HI 49152
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
 /* Ack-check kernel of hbh_bivar_ack_check_set: HBH_ACK_QUAD (k_bivar_check_quad: four lanes per ack
  * split each G1 operation, Jacobian rows -- latency), HBH_ACK_LANE (k_bivar_check: one lane per ack,

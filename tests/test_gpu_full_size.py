@@ -71,12 +71,14 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
         assert cbls.verify_g2(b["pks"][i % N], b["sigs"][i], b["hashes"][i // N]) == bool(v[i]), i
 
 
-@pytest.mark.parametrize("n", [5120, 5184, 16384, 16448], ids=["wave_max", "quad_min", "quad_max", "pair_min"])
+@pytest.mark.parametrize("n", [5120, 5184, 16384, 16448, 32768, 32832, 49152, 49216],
+                         ids=["wave_max", "quad_min", "quad_max", "pair_min", "split_lo", "split_min", "split_max",
+                              "pair2_min"])
 def test_config1_at_auto_thresholds(engine, sign_batch, n):
     """Every kernel on both sides of the AUTO boundaries (HBH_AUTO_WAVE_MAX = 5,120 checks, 80
-    documents of configs[1]; HBH_AUTO_QUAD_MAX = 16,384, 256 documents; one more document past
-    each): WAVE walks both G2 sides, QUAD and PAIR read H's line table; verdicts equal the
-    construction."""
+    documents of configs[1]; HBH_AUTO_QUAD_MAX = 16,384, 256 documents; the PAIR + QUAD split of
+    (32,768, 49,152]; one more document past each): WAVE walks both G2 sides, QUAD and PAIR read H's
+    line table; verdicts equal the construction."""
     b = sign_batch
     from hbbft_amd._lib import IMPL_PAIR, IMPL_QUAD
     for impl in (IMPL_WAVE, IMPL_QUAD, IMPL_PAIR, IMPL_AUTO):
