@@ -172,6 +172,38 @@ hbl::PairSideDesc offset_side(const hbl::PairSideDesc& d, size_t off) {
   return o;
 }
 
+// HBH_IMPL_AUTO's launches for n checks on one stream (profiles/r04/c8, c19, c20 sweeps): whole
+// rounds of HBH_AUTO_PAIR_ROUND checks (two lane-pair waves per SIMD) on PAIR, then the remainder by
+// size -- WAVE up to HBH_AUTO_WAVE_MAX, QUAD up to HBH_AUTO_QUAD_MAX, PAIR at one wave per SIMD up to
+// HBH_AUTO_SPLIT_LO, PAIR on HBH_AUTO_SPLIT_LO then QUAD on the rest up to HBH_AUTO_SPLIT_HI, PAIR.
+// A partial lane-pair round costs as much as a full one once any SIMD needs a second wave.
+hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, const hbl::PairSideDesc& s2, int flags,
+                       uint8_t* d_v, uint32_t* d_value) {
+  size_t off = 0;
+  auto at = [&](size_t o, size_t cnt, int kind) -> hipError_t {
+    const hbl::PairSideDesc a = o ? offset_side(s1, o) : s1, b = o ? offset_side(s2, o) : s2;
+    uint8_t* v = d_v ? d_v + o : nullptr;
+    uint32_t* val = d_value ? d_value + o * 144 : nullptr;
+    if (kind == HBH_IMPL_WAVE) return hbl::wave_verify(s, (int)cnt, a, b, flags, v, val);
+    if (kind == HBH_IMPL_QUAD) return hbl::quad_verify(s, (int)cnt, a, b, flags, v, val);
+    return hbl::pair_verify(s, (int)cnt, a, b, flags, v, val);
+  };
+  const size_t rounds = n > HBH_AUTO_SPLIT_HI ? n / HBH_AUTO_PAIR_ROUND : 0;
+  if (rounds) {
+    hipError_t r = at(0, rounds * HBH_AUTO_PAIR_ROUND, HBH_IMPL_PAIR);
+    if (r != hipSuccess) return r;
+    off = rounds * HBH_AUTO_PAIR_ROUND;
+  }
+  const size_t rem = n - off;
+  if (rem == 0) return hipSuccess;
+  if (rem <= HBH_AUTO_WAVE_MAX) return at(off, rem, HBH_IMPL_WAVE);
+  if (rem <= HBH_AUTO_QUAD_MAX) return at(off, rem, HBH_IMPL_QUAD);
+  if (rem <= HBH_AUTO_SPLIT_LO || rem > HBH_AUTO_SPLIT_HI) return at(off, rem, HBH_IMPL_PAIR);
+  hipError_t r = at(off, HBH_AUTO_SPLIT_LO, HBH_IMPL_PAIR);
+  if (r != hipSuccess) return r;
+  return at(off + HBH_AUTO_SPLIT_LO, rem - HBH_AUTO_SPLIT_LO, HBH_IMPL_QUAD);
+}
+
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
 // table (k_pair_prep); every other side is walked inside the verify kernel.
 int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
@@ -192,21 +224,14 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
     sd[k].qinf = (const uint8_t*)inf[k]->p;
   }
   hipEvent_t t = e->timer.begin(s, HBH_STAGE_PAIRING, e->profiling);
-  if (impl == HBH_IMPL_WAVE) {
+  if (e->impl == HBH_IMPL_AUTO)
+    HBH_CHECK(verify_auto(s, n, sd[0], sd[1], flags, d_v, d_value));
+  else if (impl == HBH_IMPL_WAVE)
     HBH_CHECK(hbl::wave_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
-  } else if (impl == HBH_IMPL_QUAD) {
+  else if (impl == HBH_IMPL_QUAD)
     HBH_CHECK(hbl::quad_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
-  } else if (e->impl == HBH_IMPL_AUTO && n > HBH_AUTO_SPLIT_LO && n <= HBH_AUTO_SPLIT_HI) {
-    // one lane-pair wave per SIMD for the first HBH_AUTO_SPLIT_LO checks, the rest (<= 16,384) on
-    // the lane-quad kernel after it: 11.5 + 7.1 ms instead of the lane pair's two-wave 20.5 ms
-    const size_t n1 = HBH_AUTO_SPLIT_LO;
-    HBH_CHECK(hbl::pair_verify(s, (int)n1, sd[0], sd[1], flags, d_v, d_value));
-    const hbl::PairSideDesc r0 = offset_side(sd[0], n1), r1 = offset_side(sd[1], n1);
-    HBH_CHECK(hbl::quad_verify(s, (int)(n - n1), r0, r1, flags, d_v ? d_v + n1 : nullptr,
-                               d_value ? d_value + n1 * 144 : nullptr));
-  } else {
+  else
     HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
-  }
   e->timer.end(s, t);
   return HBH_OK;
 }

@@ -91,6 +91,19 @@ def test_config1_at_auto_thresholds(engine, sign_batch, n):
         assert v == b["expected"][:n], impl
 
 
+@pytest.mark.parametrize("extra", [5120, 16384, 40960], ids=["wave_rest", "quad_rest", "split_rest"])
+def test_config1_auto_beyond_one_round(engine, sign_batch, extra):
+    """AUTO above 49,152 checks: one round of 65,536 on PAIR, then the remainder by size (WAVE /
+    QUAD / PAIR + QUAD) on the same stream -- the batch is configs[1] followed by its first `extra`
+    checks again; verdicts equal the construction's."""
+    b = sign_batch
+    n = NDOCS * N
+    idx = list(range(n)) + list(range(extra))
+    v = engine.verify_sig_shares([b["pks"][i % N] for i in idx], [b["sigs"][i] for i in idx], b["hashes"],
+                                 [i // N for i in idx])
+    assert v == b["expected"] + b["expected"][:extra]
+
+
 def test_config1_combines(engine, sign_batch):
     """combine_and_verify_sig for all 1,024 documents (first 22 valid shares) in one call."""
     b = sign_batch
