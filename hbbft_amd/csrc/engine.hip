@@ -174,9 +174,11 @@ hbl::PairSideDesc offset_side(const hbl::PairSideDesc& d, size_t off) {
 
 // HBH_IMPL_AUTO's launches for n checks on one stream (profiles/r04/c8, c19, c20 sweeps): whole
 // rounds of HBH_AUTO_PAIR_ROUND checks (two lane-pair waves per SIMD) on PAIR, then the remainder by
-// size -- WAVE up to HBH_AUTO_WAVE_MAX, QUAD up to HBH_AUTO_QUAD_MAX, PAIR at one wave per SIMD up to
-// HBH_AUTO_SPLIT_LO, PAIR on HBH_AUTO_SPLIT_LO then QUAD on the rest up to HBH_AUTO_SPLIT_HI, PAIR.
-// A partial lane-pair round costs as much as a full one once any SIMD needs a second wave.
+// size -- above HBH_AUTO_SPLIT_HI one more (partial) PAIR round; above HBH_AUTO_SPLIT_LO PAIR on
+// HBH_AUTO_SPLIT_LO checks (one wave per SIMD) first; what is left runs on WAVE up to
+// HBH_AUTO_WAVE_MAX, QUAD up to HBH_AUTO_QUAD_MAX, PAIR (one wave per SIMD) above.  A partial
+// lane-pair round costs as much as a full one once any SIMD needs a second wave (40,960 checks:
+// PAIR alone 20.5-20.7 ms, PAIR + QUAD 19.4 ms, profiles/r04/c20_auto_split.txt).
 hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, const hbl::PairSideDesc& s2, int flags,
                        uint8_t* d_v, uint32_t* d_value) {
   size_t off = 0;
@@ -188,20 +190,25 @@ hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, con
     if (kind == HBH_IMPL_QUAD) return hbl::quad_verify(s, (int)cnt, a, b, flags, v, val);
     return hbl::pair_verify(s, (int)cnt, a, b, flags, v, val);
   };
-  const size_t rounds = n > HBH_AUTO_SPLIT_HI ? n / HBH_AUTO_PAIR_ROUND : 0;
-  if (rounds) {
-    hipError_t r = at(0, rounds * HBH_AUTO_PAIR_ROUND, HBH_IMPL_PAIR);
-    if (r != hipSuccess) return r;
-    off = rounds * HBH_AUTO_PAIR_ROUND;
+  if (n > HBH_AUTO_SPLIT_HI) {  // whole two-wave lane-pair rounds
+    off = (n / HBH_AUTO_PAIR_ROUND) * HBH_AUTO_PAIR_ROUND;
+    if (off) {
+      const hipError_t r = at(0, off, HBH_IMPL_PAIR);
+      if (r != hipSuccess) return r;
+    }
   }
-  const size_t rem = n - off;
+  size_t rem = n - off;
   if (rem == 0) return hipSuccess;
+  if (rem > HBH_AUTO_SPLIT_HI) return at(off, rem, HBH_IMPL_PAIR);  // one partial two-wave round
+  if (rem > HBH_AUTO_SPLIT_LO) {  // one lane-pair wave per SIMD, then the rest by size
+    const hipError_t r = at(off, HBH_AUTO_SPLIT_LO, HBH_IMPL_PAIR);
+    if (r != hipSuccess) return r;
+    off += HBH_AUTO_SPLIT_LO;
+    rem -= HBH_AUTO_SPLIT_LO;
+  }
   if (rem <= HBH_AUTO_WAVE_MAX) return at(off, rem, HBH_IMPL_WAVE);
   if (rem <= HBH_AUTO_QUAD_MAX) return at(off, rem, HBH_IMPL_QUAD);
-  if (rem <= HBH_AUTO_SPLIT_LO || rem > HBH_AUTO_SPLIT_HI) return at(off, rem, HBH_IMPL_PAIR);
-  hipError_t r = at(off, HBH_AUTO_SPLIT_LO, HBH_IMPL_PAIR);
-  if (r != hipSuccess) return r;
-  return at(off + HBH_AUTO_SPLIT_LO, rem - HBH_AUTO_SPLIT_LO, HBH_IMPL_QUAD);
+  return at(off, rem, HBH_IMPL_PAIR);
 }
 
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line

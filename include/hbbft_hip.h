@@ -311,9 +311,9 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
  *     checks WAVE 5.3 / QUAD 7.0 / PAIR 10.6; 8,192: 10.2 / 7.0 / 10.7; 16,384: 20.1 / 7.1 / 11.1;
  *     24,576: QUAD 14.3 (two rounds of waves) / PAIR 11.2.  Between 32,768 and 49,152 checks the lane
  *     pair needs a second wave on some SIMDs (40,960: 20.5 ms), so AUTO runs the first 32,768 on
- *     PAIR (one wave per SIMD, 11.5 ms) and the rest on QUAD (7.1 ms) on the same stream; above
- *     49,152, whole rounds of 65,536 checks (two lane-pair waves per SIMD) run on PAIR and the
- *     remainder follows the rules above.
+ *     PAIR (one wave per SIMD, 11.5 ms) and the rest by the rules above (WAVE / QUAD) on the same
+ *     stream; above 49,152, whole rounds of 65,536 checks (two lane-pair waves per SIMD) run on
+ *     PAIR and the remainder follows the same rules.
  * Retired (selecting them returns HBH_ERR_ARG): HBH_IMPL_THREAD (0, round 1's one-thread kernel),
  * HBH_IMPL_LANE_COOP (1, six lanes per check) and HBH_IMPL_THREAD_SIGNED (2, one thread per check
  * on signed limbs) -- WAVE and PAIR cover every batch size faster. */
@@ -326,7 +326,7 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_QUAD 6
 #define HBH_AUTO_WAVE_MAX 5120
 #define HBH_AUTO_QUAD_MAX 16384
-#define HBH_AUTO_SPLIT_LO 32768  /* AUTO: (32,768, 49,152] checks = PAIR on 32,768 + QUAD on the rest */
+#define HBH_AUTO_SPLIT_LO 32768  /* AUTO: (32,768, 49,152] checks = PAIR on 32,768 + the rest by size */
 #define HBH_AUTO_SPLIT_HI 49152
 #define HBH_AUTO_PAIR_ROUND 65536  /* AUTO above HBH_AUTO_SPLIT_HI: whole rounds of 65,536 on PAIR, the rest by size */
 int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
