@@ -1050,8 +1050,10 @@ def run_epoch_bench(args, eng, world, rank, dev):
         if args.pipeline:
             host_gpu["pipelined_ms"] = {k: sum(r.overlap.get(k, 0.0) for r in results) / len(results) * 1e3
                                         for k in ("hand_s", "worker_engine_s")}
-        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (5,120) checks -- the epoch's -- to the wave kernel.
-        main_k = roofline_entry("hbs::k_wave", pair_n, pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
+        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (5,120) checks to the wave kernel and the larger
+        # ones (<= 16,384: the coin phase's first window) to the lane-quad kernel; the stage time is both
+        main_k = roofline_entry("hbs::k_wave + hbs::k_quad_verify (AUTO by drain size)", pair_n,
+                                pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
                                 workcount.PAIR_CHECK_WALK, "share / ciphertext check")
         line = {
             "metric": "HoneyBadger epochs/sec, one node's threshold crypto, N=100 f=33", "value": world * 1e3 / ms,
@@ -1072,6 +1074,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
             "engine_calls_per_epoch": sum(r.engine_calls for r in results) / len(results),
             "checks_drained_per_epoch": drained / len(results), "checks_consumed_per_epoch": consumed,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)", traffic=None,
+                             traffic_note="the drains mix two kernels at varying sizes; their per-launch HBM is in "
+                                          "profiles/r04/pmc_traffic.json (by_source wave4k: k_wave 4,096 checks, "
+                                          "quad16k: k_quad_verify 16,384 checks)",
                              note="drains of different sizes (a few thousand checks, 100 ciphertexts, 100 master "
                                   "verifies) run below one wave per SIMD: latency-bound; no single occupancy ceiling"),
         }
