@@ -44,12 +44,13 @@ ACK_LANE_MIN = 65536                            # HBH_ACK_LANE_MIN (include/hbbf
 MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
-IMPLS = {"auto": 3, "pair": 4, "wave": 5, "quad": 6}   # HBH_IMPL_* (include/hbbft_hip.h)
+IMPLS = {"auto": 3, "pair": 4, "wave": 5, "quad": 6, "oct": 7}   # HBH_IMPL_* (include/hbbft_hip.h)
 PAIR_SIGN = "hbs::k_pair_verify<false, true, 2>"
 PAIR_DECRYPT = "hbs::k_pair_verify<false, false, 0>"
 KERNEL_NAMES = {"pair": PAIR_SIGN,
                 "wave": "hbs::k_wave (one wave per check)",
                 "quad": "hbs::k_quad_verify<false, true, 2>",
+                "oct": "hbs::k_oct_verify<false, true, 2>",
                 "auto": PAIR_SIGN,
                 "decrypt": PAIR_DECRYPT}
 G1_UNC = bytes.fromhex(
@@ -260,8 +261,9 @@ def reference_work(main_k, workcount):
 
 
 def pair_waves_per_simd(checks, lanes=2):
-    """Waves per SIMD of the lane-pair kernel k_pair_verify (two lanes per check) or the lane-quad
-    kernel k_quad_verify (lanes=4): 64-lane waves, 1,024 SIMDs."""
+    """Waves per SIMD of the lane-pair kernel k_pair_verify (two lanes per check), the lane-quad
+    kernel k_quad_verify (lanes=4) or the lane-octo kernel k_oct_verify (lanes=8): 64-lane waves,
+    1,024 SIMDs."""
     w = checks * lanes / 64 / 1024
     return 2 if w >= 2 else (1 if w >= 1 else round(w, 3))
 
@@ -437,7 +439,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
-    ap.add_argument("--impl", choices=["pair", "wave", "quad", "auto"], default="auto",
+    ap.add_argument("--impl", choices=["pair", "wave", "quad", "oct", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
@@ -548,11 +550,11 @@ def main():
     if rank == 0:
         kern_ms = pair_ms / max(pair_n, 1)
         main_k = roofline_entry(KERNEL_NAMES[args.impl], pair_n, kern_ms, n, workcount.PAIR_CHECK_WALK, "share check",
-                                pair_waves_per_simd(n, 4 if args.impl == "quad" else 2)
-                                if args.impl in ("pair", "auto", "quad") else None)
+                                pair_waves_per_simd(n, {"quad": 4, "oct": 8}.get(args.impl, 2))
+                                if args.impl in ("pair", "auto", "quad", "oct") else None)
         kernels = [main_k]
         if prep_n:
-            kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto", "quad") else "hb::k_g2_prepare",
+            kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto", "quad", "oct") else "hb::k_g2_prepare",
                                           prep_n, prep_ms / prep_n, nh, workcount.PAIR_PREP_DOC, "document (G2 walk)",
                                           nh * 4 / 64 / 1024))  # one lane quad per point
         out = {
@@ -1050,9 +1052,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
         if args.pipeline:
             host_gpu["pipelined_ms"] = {k: sum(r.overlap.get(k, 0.0) for r in results) / len(results) * 1e3
                                         for k in ("hand_s", "worker_engine_s")}
-        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (5,120) checks to the wave kernel and the larger
-        # ones (<= 16,384: the coin phase's first window) to the lane-quad kernel; the stage time is both
-        main_k = roofline_entry("hbs::k_wave + hbs::k_quad_verify (AUTO by drain size)", pair_n,
+        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (4,096) checks to the wave kernel, <= 8,192 (the
+        # window) to the lane-octo kernel and larger ones to the lane quad; the stage time is all of them
+        main_k = roofline_entry("hbs::k_wave + hbs::k_oct_verify (AUTO by drain size)", pair_n,
                                 pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
                                 workcount.PAIR_CHECK_WALK, "share / ciphertext check")
         line = {
@@ -1074,9 +1076,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
             "engine_calls_per_epoch": sum(r.engine_calls for r in results) / len(results),
             "checks_drained_per_epoch": drained / len(results), "checks_consumed_per_epoch": consumed,
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)", traffic=None,
-                             traffic_note="the drains mix two kernels at varying sizes; their per-launch HBM is in "
+                             traffic_note="the drains mix kernels at varying sizes; their per-launch HBM is in "
                                           "profiles/r04/pmc_traffic.json (by_source wave4k: k_wave 4,096 checks, "
-                                          "quad16k: k_quad_verify 16,384 checks)",
+                                          "oct8k: k_oct_verify 8,192 checks, quad16k: k_quad_verify 16,384 checks)",
                              note="drains of different sizes (a few thousand checks, 100 ciphertexts, 100 master "
                                   "verifies) run below one wave per SIMD: latency-bound; no single occupancy ceiling"),
         }

@@ -83,7 +83,7 @@ SIGNATURES = [
     ("hbh_encrypt", _I, [_SZ, _P, _I, _P, _P, _P, _P, _P, _P, _I]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
-IMPL_AUTO, IMPL_PAIR, IMPL_WAVE, IMPL_QUAD = 3, 4, 5, 6   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)
+IMPL_AUTO, IMPL_PAIR, IMPL_WAVE, IMPL_QUAD, IMPL_OCT = 3, 4, 5, 6, 7   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)
 ACK_AUTO, ACK_QUAD, ACK_LANE = 0, 1, 2        # HBH_ACK_*
 
 _lib = None

@@ -155,7 +155,9 @@ int end_call(hbh_engine* e, hipStream_t s) {
 
 int resolve_impl(const hbh_engine* e, size_t n) {
   if (e->impl != HBH_IMPL_AUTO) return e->impl;
-  return n <= HBH_AUTO_WAVE_MAX ? HBH_IMPL_WAVE : (n <= HBH_AUTO_QUAD_MAX ? HBH_IMPL_QUAD : HBH_IMPL_PAIR);
+  if (n <= HBH_AUTO_WAVE_MAX) return HBH_IMPL_WAVE;
+  if (n <= HBH_AUTO_OCT_MAX) return HBH_IMPL_OCT;
+  return n <= HBH_AUTO_QUAD_MAX ? HBH_IMPL_QUAD : HBH_IMPL_PAIR;
 }
 
 // the checks [off, n) of a side: per-check P and index map (or per-check Q when there is no map)
@@ -176,7 +178,8 @@ hbl::PairSideDesc offset_side(const hbl::PairSideDesc& d, size_t off) {
 // rounds of HBH_AUTO_PAIR_ROUND checks (two lane-pair waves per SIMD) on PAIR, then the remainder by
 // size -- above HBH_AUTO_SPLIT_HI one more (partial) PAIR round; above HBH_AUTO_SPLIT_LO PAIR on
 // HBH_AUTO_SPLIT_LO checks (one wave per SIMD) first; what is left runs on WAVE up to
-// HBH_AUTO_WAVE_MAX, QUAD up to HBH_AUTO_QUAD_MAX, PAIR (one wave per SIMD) above.  A partial
+// HBH_AUTO_WAVE_MAX, OCT up to HBH_AUTO_OCT_MAX, QUAD up to HBH_AUTO_QUAD_MAX, PAIR (one wave per
+// SIMD) above.  A partial
 // lane-pair round costs as much as a full one once any SIMD needs a second wave (40,960 checks:
 // PAIR alone 20.5-20.7 ms, PAIR + QUAD 19.4 ms, profiles/r04/c20_auto_split.txt).
 hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, const hbl::PairSideDesc& s2, int flags,
@@ -188,6 +191,7 @@ hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, con
     uint32_t* val = d_value ? d_value + o * 144 : nullptr;
     if (kind == HBH_IMPL_WAVE) return hbl::wave_verify(s, (int)cnt, a, b, flags, v, val);
     if (kind == HBH_IMPL_QUAD) return hbl::quad_verify(s, (int)cnt, a, b, flags, v, val);
+    if (kind == HBH_IMPL_OCT) return hbl::oct_verify(s, (int)cnt, a, b, flags, v, val);
     return hbl::pair_verify(s, (int)cnt, a, b, flags, v, val);
   };
   if (n > HBH_AUTO_SPLIT_HI) {  // whole two-wave lane-pair rounds
@@ -207,6 +211,7 @@ hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, con
     rem -= HBH_AUTO_SPLIT_LO;
   }
   if (rem <= HBH_AUTO_WAVE_MAX) return at(off, rem, HBH_IMPL_WAVE);
+  if (rem <= HBH_AUTO_OCT_MAX) return at(off, rem, HBH_IMPL_OCT);
   if (rem <= HBH_AUTO_QUAD_MAX) return at(off, rem, HBH_IMPL_QUAD);
   return at(off, rem, HBH_IMPL_PAIR);
 }
@@ -237,6 +242,8 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
     HBH_CHECK(hbl::wave_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   else if (impl == HBH_IMPL_QUAD)
     HBH_CHECK(hbl::quad_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  else if (impl == HBH_IMPL_OCT)
+    HBH_CHECK(hbl::oct_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   else
     HBH_CHECK(hbl::pair_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   e->timer.end(s, t);
@@ -476,7 +483,8 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
-  if (impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO && impl != HBH_IMPL_WAVE && impl != HBH_IMPL_QUAD)
+  if (impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO && impl != HBH_IMPL_WAVE && impl != HBH_IMPL_QUAD &&
+      impl != HBH_IMPL_OCT)
     return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;

@@ -38,6 +38,12 @@ hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairS
 hipError_t quad_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
                        uint8_t* verdict, uint32_t* value_out);
 
+// --------------------------------------------------------------- lane-octo pairing (k_oct.hpp)
+// The same with EIGHT lanes per check (four lane pairs, four products per round): one wave per SIMD
+// at 8,192 checks.
+hipError_t oct_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
+                      uint8_t* verdict, uint32_t* value_out);
+
 // --------------------------------------------------------------- wave-per-check pairing (k_wave.hip)
 // The same verdicts / values as pair_verify with one 64-lane workgroup per check (the latency
 // kernel: a check's Fp2 products run on 32 lane pairs side by side).  TABLE sides read pair_prep

@@ -322,10 +322,11 @@ class Engine:
                                               vp(d_verdicts)))
 
     def set_pairing_impl(self, impl):
-        """HBH_IMPL_*: 3 = auto (default: wave up to HBH_AUTO_WAVE_MAX checks, lane quad up to
-        HBH_AUTO_QUAD_MAX, lane pair above),
+        """HBH_IMPL_*: 3 = auto (default: wave up to HBH_AUTO_WAVE_MAX checks, lane octo up to
+        HBH_AUTO_OCT_MAX, lane quad up to HBH_AUTO_QUAD_MAX, lane pair above),
         4 = lane pair (two lanes per check, fused), 5 = wave (one 64-lane wave per check: the latency
-        kernel), 6 = lane quad (four lanes per check: mid-size batches).  0, 1, 2 are retired
+        kernel), 6 = lane quad (four lanes per check: mid-size batches), 7 = lane octo (eight lanes per
+        check).  0, 1, 2 are retired
         implementations (HBH_ERR_ARG)."""
         check(self._l.hbh_engine_set_pairing_impl(self._h, int(impl)))
 

@@ -305,13 +305,17 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
  *   HBH_IMPL_QUAD (k_quad.hip): FOUR lanes per check -- two lane pairs holding the check's state
  *     side by side and splitting each step's independent products (k_pair's work per check in
  *     ~0.55 of its per-lane time).  Mid-size path: 16,384 checks are one wave per SIMD.
- *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, QUAD up to
- *     HBH_AUTO_QUAD_MAX (one wave per SIMD), PAIR above -- the measured crossovers
- *     (profiles/r04/c8_sweep_wave_quad_pair.txt, kernel ms per call on the sign workload): 4,096
- *     checks WAVE 5.3 / QUAD 7.0 / PAIR 10.6; 8,192: 10.2 / 7.0 / 10.7; 16,384: 20.1 / 7.1 / 11.1;
- *     24,576: QUAD 14.3 (two rounds of waves) / PAIR 11.2.  Between 32,768 and 49,152 checks the lane
+ *   HBH_IMPL_OCT (k_oct.hpp): EIGHT lanes per check -- four lane pairs, four independent products per
+ *     round.  Small-batch path: 8,192 checks are one wave per SIMD.
+ *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, OCT up to
+ *     HBH_AUTO_OCT_MAX, QUAD up to HBH_AUTO_QUAD_MAX (each one wave per SIMD at its maximum), PAIR
+ *     above -- the measured crossovers (profiles/r04/c8_sweep_wave_quad_pair.txt,
+ *     c23_oct_wave_sweep.txt, kernel ms per call on the sign workload): 4,096 checks WAVE 5.3 /
+ *     OCT 5.5 / QUAD 7.0 / PAIR 10.6; 4,608: WAVE 6.6 / OCT 5.5; 8,192: 10.2 / 5.5 / 7.0 / 10.7;
+ *     16,384: WAVE 20.1 / OCT 11.6 / QUAD 7.1 / PAIR 11.1; 24,576: QUAD 14.3 (two rounds of waves) /
+ *     PAIR 11.2.  Between 32,768 and 49,152 checks the lane
  *     pair needs a second wave on some SIMDs (40,960: 20.5 ms), so AUTO runs the first 32,768 on
- *     PAIR (one wave per SIMD, 11.5 ms) and the rest by the rules above (WAVE / QUAD) on the same
+ *     PAIR (one wave per SIMD, 11.5 ms) and the rest by the rules above (WAVE / OCT / QUAD) on the same
  *     stream; above 49,152, whole rounds of 65,536 checks (two lane-pair waves per SIMD) run on
  *     PAIR and the remainder follows the same rules.
  * Retired (selecting them returns HBH_ERR_ARG): HBH_IMPL_THREAD (0, round 1's one-thread kernel),
@@ -324,7 +328,9 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
 #define HBH_IMPL_PAIR 4
 #define HBH_IMPL_WAVE 5
 #define HBH_IMPL_QUAD 6
-#define HBH_AUTO_WAVE_MAX 5120
+#define HBH_IMPL_OCT 7
+#define HBH_AUTO_WAVE_MAX 4096
+#define HBH_AUTO_OCT_MAX 8192
 #define HBH_AUTO_QUAD_MAX 16384
 #define HBH_AUTO_SPLIT_LO 32768  /* AUTO: (32,768, 49,152] checks = PAIR on 32,768 + the rest by size */
 #define HBH_AUTO_SPLIT_HI 49152

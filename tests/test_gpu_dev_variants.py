@@ -169,9 +169,9 @@ def test_dev_calls_on_two_streams(engine, impl):
         engine.set_pairing_impl(IMPL_AUTO)
 
 
-@pytest.mark.parametrize("impl", [4, 5, 6], ids=["pair", "wave", "quad"])
+@pytest.mark.parametrize("impl", [4, 5, 6, 7], ids=["pair", "wave", "quad", "oct"])
 def test_dev_index_out_of_range_rejects(engine, impl):
-    """HBH_IMPL_PAIR, HBH_IMPL_WAVE and HBH_IMPL_QUAD validate device index arrays in-kernel: an index >= its table
+    """HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD and HBH_IMPL_OCT validate device index arrays in-kernel: an index >= its table
     size gives verdict 0 for that item only (never a read past the table)."""
     from hbbft_amd._lib import IMPL_AUTO
     rng = random.Random(9)

@@ -13,9 +13,9 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[4, 5, 6, 3], ids=["pair", "wave", "quad", "auto"])
+@pytest.fixture(params=[4, 5, 6, 7, 3], ids=["pair", "wave", "quad", "oct", "auto"])
 def eng(engine, request):
-    """Every pairing implementation (HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD) and the default
+    """Every pairing implementation (HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD, HBH_IMPL_OCT) and the default
     HBH_IMPL_AUTO must give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine

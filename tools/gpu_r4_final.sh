@@ -23,8 +23,8 @@ cd /tmp
 B="$R/bench.py --steps 5 --warmup 2"
 mkdir -p $O/default_bench
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/default_bench -o run -- python3 $B > $O/default_bench/run.log 2>&1 || { echo "default trace failed"; tail -5 $O/default_bench/run.log; exit 1; }
-# PMC passes: name:bench arguments (quad16k / wave4k: the mid-size and epoch-size pairing kernels)
-for S in ${PMC_SETS:-"sign:--workload sign" "decrypt:--workload decrypt" "dkg:--workload dkg" "quad16k:--workload sign --impl quad --batch 16384" "wave4k:--workload sign --impl wave --batch 4096"}; do
+# PMC passes: name:bench arguments (quad16k / oct8k / wave4k: the mid-size and epoch-size pairing kernels)
+for S in ${PMC_SETS:-"sign:--workload sign" "decrypt:--workload decrypt" "dkg:--workload dkg" "quad16k:--workload sign --impl quad --batch 16384" "oct8k:--workload sign --impl oct --batch 8192" "wave4k:--workload sign --impl wave --batch 4096"}; do
   W=${S%%:*}; A=${S#*:}
   P=$O/pmc_$W
   mkdir -p $P
