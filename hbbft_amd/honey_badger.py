@@ -615,7 +615,11 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                     ver.queue_sig(keys.pks[j], hmap[(p, e)], ba.shares[(p, e, j)])
                     queued_n[(p, e)] = c + 1
 
+    sig_cache, ni_index, ni_pks, ni_t = ver._sig, ni._index, ni.pk_shares, ni.t
+
     def hand_window(batch, end):
+        shares = ba.shares
+        t_msgs = time.perf_counter()
         for m in batch:
             p, e, j = m
             b = bas[p]
@@ -625,6 +629,33 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
             be = b.epoch
             if b.decision is not None or e < be or (e == be and (b.coin_decided or b.pending is not None)):
                 continue
+            # The two outcomes most messages have, as BinaryAgreementCoin.handle_message would reach
+            # them, without its call chain and empty Steps: a future epoch's share stored in the
+            # incoming queue (first from this sender), and a current-epoch share with a cached valid
+            # verdict that leaves the coin below t + 1 shares.  Everything else (faults, a share that
+            # completes the coin, a verdict not cached) takes the full path below.
+            share = shares[m]
+            if e > be:
+                if e <= be + b.max_future_epochs:
+                    q = b.incoming.get(e)
+                    if q is None:
+                        q = b.incoming[e] = {}
+                    if j not in q and type(share) is bytes:
+                        q[j] = share
+                        b.queued += 1
+                        continue
+            else:
+                ts = b.ts
+                rs = ts.received_shares
+                h = ts.doc_hash
+                if not ts.terminated and h is not None and j not in rs and len(rs) < ni_t:
+                    idx, pk = ni_index.get(j), ni_pks.get(j)
+                    d = sig_cache.get(h)
+                    if (idx is not None and type(pk) is bytes and type(share) is bytes and d is not None
+                            and d.get((pk, share)) is True):
+                        ver.lookups += 1
+                        rs[j] = (idx, share)
+                        continue
             try:
                 step = b.handle_message(j, e, ba.shares[m])
             except ProtocolError as err:
@@ -632,6 +663,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                 continue
             if step.fault_log or step.output:
                 record(p, step)
+        res.timing["coin_messages"] = res.timing.get("coin_messages", 0.0) + time.perf_counter() - t_msgs
         resolve()
         local_events(end)
         resolve()
@@ -766,12 +798,24 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
 
     handed_dec = {p: handed.setdefault(("dec", p), []) for p in td}
 
+    dec_cache, dni_index, dni_pks, dni_t = ver._dec, ni_dec._index, ni_dec.pk_shares, ni_dec.t
+
     def hand_dec(p, j):
         handed_dec[p].append(j)
         inst = td[p]
         if inst.terminated:  # handle_message of a terminated instance is an empty Step (:183-185)
             return _EMPTY
-        return inst.handle_message(j, dec_sh[(p, j)])
+        share = dec_sh[(p, j)]
+        # the outcome most shares have, as ThresholdDecrypt.handle_message would reach it: a cached
+        # valid verdict from a new sender that leaves the instance below t + 1 shares (the rest, full path)
+        ct, sh = inst.ciphertext, inst.shares
+        if ct is not None and j not in sh and len(sh) < dni_t and type(share) is bytes:
+            idx, pk, d = dni_index.get(j), dni_pks.get(j), dec_cache.get((ct.huv, ct.w))
+            if idx is not None and type(pk) is bytes and d is not None and d.get((pk, share)) is True:
+                ver.lookups += 1
+                sh[j] = (idx, share)
+                return _EMPTY
+        return inst.handle_message(j, share)
 
     dec_msgs = [m for m in trace.dec_msgs if m[0] in td]  # (shares of a faulted contribution: no instance)
     for p, out in _deliver(ver, dec_msgs, window, td,

@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--no-preverify", action="store_true")
     ap.add_argument("--window", type=int, default=8192)
     ap.add_argument("--device-ms", default="0,0", help="emulated device time per drain: base ms, ms per check")
+    ap.add_argument("--dump", default=None, metavar="FILE",
+                    help="write a digest of the last epoch's outputs (decisions, coins, plaintexts, faults, errors) "
+                         "to compare two versions of the flows")
     args = ap.parse_args()
     eng = HostEngine()
     b, per = (float(x) for x in args.device_ms.split(","))
@@ -140,6 +143,23 @@ def main():
               "faults", len(res.faults), "errors", len(res.errors), flush=True)
         if pr:
             pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+    if args.dump:
+        with open(args.dump, "w") as f:
+            f.write(digest(res))
+
+
+def digest(res):
+    """Canonical text of an epoch's observable outputs."""
+    import hashlib
+    lines = ["decisions %r" % sorted(res.ba_decisions.items()),
+             "ba_coins %r" % sorted((p, sorted(c.items())) for p, c in res.ba_coins.items()),
+             "coins %r" % sorted(res.coins.items()),
+             "signatures %s" % hashlib.sha256(b"".join(bytes(res.signatures[p]) for p in sorted(res.signatures))).hexdigest(),
+             "plaintexts %s" % hashlib.sha256(b"".join(bytes(res.plaintexts[p]) for p in sorted(res.plaintexts))).hexdigest(),
+             "faults %r" % sorted(repr(f) for f in res.faults),
+             "errors %r" % sorted(repr(e) for e in res.errors),
+             "ba_queued %r" % res.ba_queued]
+    return "\n".join(lines) + "\n"
 
 
 if __name__ == "__main__":
