@@ -96,6 +96,23 @@ class BinaryAgreementCoin:
             raise ProtocolError("HandleThresholdSign", e.kind)
         return self._on_coin_step(ts_step)
 
+    def _store_valid_share(self, sender, share):
+        """_handle_coin's most common outcome without its call chain and empty Steps: a share with a
+        cached valid verdict from a new sender that leaves the coin below t + 1 shares is stored in
+        the ThresholdSign (threshold_sign.rs:181-197).  False: nothing done, take the full path."""
+        if self.coin_decided or self.pending is not None:
+            return False
+        ts, ni = self.ts, self.netinfo
+        rs, h = ts.received_shares, ts.doc_hash
+        if ts.terminated or h is None or sender in rs or len(rs) >= ni.t or type(share) is not bytes:
+            return False
+        idx, pk, d = ni._index.get(sender), ni.pk_shares.get(sender), self.verifier._sig.get(h)
+        if idx is None or type(pk) is not bytes or d is None or d.get((pk, share)) is not True:
+            return False
+        self.verifier.lookups += 1
+        rs[sender] = (idx, share)
+        return True
+
     def _on_coin_step(self, ts_step):  # :394-405
         epoch = self.epoch
         step = Step(fault_log=[Fault(f.node_id, "CoinFault:" + f.kind) for f in ts_step.fault_log],
@@ -193,6 +210,8 @@ class BinaryAgreementCoin:
             if queued:
                 self.verifier.drain()
         for sender, share in replay:
+            if self._store_valid_share(sender, share):
+                continue
             step.extend(self._handle_coin(sender, share))
             if self.decision is not None:
                 return step

@@ -603,19 +603,29 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                     except ProtocolError as err:
                         res.errors.append(("coin", p, err))
 
+    sig_cache, ni_index, ni_pks, ni_t = ver._sig, ni._index, ni.pk_shares, ni.t
+
+    pks = keys.pks
+
     def queue_window(batch):
-        for p, e, j in batch:
+        shares, qsig = ba.shares, ver._qsig  # (a drain replaces ver._qsig; none runs in here)
+        for m in batch:
+            p, e, j = m
             b = bas[p]
             if b.decision is None and e >= b.epoch and (b.epoch < e or not b.coin_decided):
                 # a current epoch's shares are read in arrival order: the first t + 1 + slack; a
                 # future epoch's are replayed in sender order (binary_agreement.rs:507-519), so
                 # all of them are pre-verified
-                c = queued_n.get((p, e), 0)
+                pe = (p, e)
+                c = queued_n.get(pe, 0)
                 if limit is None or c < limit or e > b.epoch:
-                    ver.queue_sig(keys.pks[j], hmap[(p, e)], ba.shares[(p, e, j)])
-                    queued_n[(p, e)] = c + 1
-
-    sig_cache, ni_index, ni_pks, ni_t = ver._sig, ni._index, ni.pk_shares, ni.t
+                    pk, h, sh = pks[j], hmap[pe], shares[m]
+                    if type(pk) is bytes and type(h) is bytes and type(sh) is bytes:  # queue_sig inlined
+                        if (pk, sh) not in sig_cache.get(h, ()):
+                            qsig.append((pk, h, sh))
+                    else:
+                        ver.queue_sig(pk, h, sh)
+                    queued_n[pe] = c + 1
 
     def hand_window(batch, end):
         shares = ba.shares
@@ -663,10 +673,17 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                 continue
             if step.fault_log or step.output:
                 record(p, step)
-        res.timing["coin_messages"] = res.timing.get("coin_messages", 0.0) + time.perf_counter() - t_msgs
+        t1 = time.perf_counter()
+        tm = res.timing
+        tm["coin_messages"] = tm.get("coin_messages", 0.0) + t1 - t_msgs
         resolve()
+        t2 = time.perf_counter()
         local_events(end)
+        t3 = time.perf_counter()
         resolve()
+        t4 = time.perf_counter()
+        tm["coin_resolve"] = tm.get("coin_resolve", 0.0) + (t2 - t1) + (t4 - t3)
+        tm["coin_local"] = tm.get("coin_local", 0.0) + t3 - t2
 
     local_events(0)
     resolve()
@@ -677,7 +694,9 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
     prev = None
     for w0 in range(0, len(msgs), window):
         batch = msgs[w0:w0 + window]
+        t_q = time.perf_counter()
         queue_window(batch)
+        res.timing["coin_queue"] = res.timing.get("coin_queue", 0.0) + time.perf_counter() - t_q
         if not pipelined:
             ver.drain()
             if after_first_drain is not None:
