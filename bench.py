@@ -443,9 +443,9 @@ def main():
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
-    ap.add_argument("--window", type=int, default=8192,
-                    help="epoch workload: messages per verifier drain (8,192: 5 engine calls per epoch; 4,096: 9, "
-                         "15.1 vs 12.4 epochs/s, profiles/r04/c12_epoch_windows.txt)")
+    ap.add_argument("--window", type=int, default=6144,
+                    help="epoch workload: messages per verifier drain (6,144: 5 engine calls per epoch, 18.3-21.6 "
+                         "epochs/s; 8,192: 18.5-19.4; 4,096: 8 calls, 15.9-18.9; profiles/r04/c27_*, c28_*)")
     ap.add_argument("--epoch-coins", choices=["ba", "synthetic"], default="ba",
                     help="epoch workload: coins from Binary Agreement instances or one ThresholdSign each")
     ap.add_argument("--ack-impl", choices=["auto", "quad", "lane"], default="auto",
@@ -1052,8 +1052,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
         if args.pipeline:
             host_gpu["pipelined_ms"] = {k: sum(r.overlap.get(k, 0.0) for r in results) / len(results) * 1e3
                                         for k in ("hand_s", "worker_engine_s")}
-        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (4,096) checks to the wave kernel, <= 8,192 (the
-        # window) to the lane-octo kernel and larger ones to the lane quad; the stage time is all of them
+        # AUTO sends drains of <= HBH_AUTO_WAVE_MAX (4,096) checks to the wave kernel, <= 8,192 to the
+        # lane-octo kernel and larger ones to the lane quad; the stage time is all of them
         main_k = roofline_entry("hbs::k_wave + hbs::k_oct_verify (AUTO by drain size)", pair_n,
                                 pair_ms / max(pair_n, 1), drained / max(pair_n, 1),
                                 workcount.PAIR_CHECK_WALK, "share / ciphertext check")

@@ -350,7 +350,7 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
         yield from hand(prev)
 
 
-def run_epoch(engine, keys, trace, window=8192, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
+def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
               defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;

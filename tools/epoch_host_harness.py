@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--prefetch", action="store_true", help="coin documents prefetched (here: same epoch)")
     ap.add_argument("--pipeline", action="store_true")
     ap.add_argument("--no-preverify", action="store_true")
-    ap.add_argument("--window", type=int, default=8192)
+    ap.add_argument("--window", type=int, default=6144)
     ap.add_argument("--device-ms", default="0,0", help="emulated device time per drain: base ms, ms per check")
     ap.add_argument("--dump", default=None, metavar="FILE",
                     help="write a digest of the last epoch's outputs (decisions, coins, plaintexts, faults, errors) "
