@@ -23,6 +23,7 @@ import os
 import random
 import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -443,6 +444,10 @@ def main():
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
+    ap.add_argument("--prefetch-early", action="store_true",
+                    help="epoch workload: start the next epoch's coin prefetch with the epoch, beside the decryption prep")
+    ap.add_argument("--preverify-at", choices=["first_drain", "start"], default="first_drain",
+                    help="epoch workload: when the decryption-share pre-verification starts")
     ap.add_argument("--window", type=int, default=6144,
                     help="epoch workload: messages per verifier drain (6,144: 5 engine calls per epoch, 18.3-21.6 "
                          "epochs/s; 8,192: 18.5-19.4; 4,096: 8 calls, 15.9-18.9; profiles/r04/c27_*, c28_*)")
@@ -992,11 +997,26 @@ def run_epoch_bench(args, eng, world, rank, dev):
         return prefetch_coins(keys, traces[k].hb_epoch, range(n)) if pf_on else None
 
     pf = prefetch(0)
-    for k, tr in enumerate(traces[:args.warmup]):
-        nxt = prefetch(k + 1)
+
+    def epoch_with_prefetch(k, tr, pf):
+        # the next epoch's coin prefetch starts once this epoch's decryption prep has the host threads
+        # to itself (after_prep), unless --prefetch-early
+        box, ev = [], threading.Event()
+
+        def start_next():
+            box.append(prefetch(k + 1))
+            ev.set()
+
+        if args.prefetch_early:
+            start_next()
         r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf,
-                      preverify=not args.no_preverify)
-        pf = nxt
+                      preverify=not args.no_preverify, preverify_at=args.preverify_at,
+                      after_prep=None if args.prefetch_early else start_next)
+        ev.wait()  # (the prep's done-callback may still be running on its pool thread)
+        return r, box[0]
+
+    for k, tr in enumerate(traces[:args.warmup]):
+        r, pf = epoch_with_prefetch(k, tr, pf)
         ok = ok and r.plaintexts == tr.proposals
     if world > 1:
         dist.barrier()
@@ -1014,10 +1034,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
         prof.enable()
     t0 = time.perf_counter()
     for k in range(args.warmup, len(traces) - 1):
-        nxt = prefetch(k + 1)
-        results.append(run_epoch(eng, keys, traces[k], window=args.window, pipelined=args.pipeline, coin_prefetch=pf,
-                                 preverify=not args.no_preverify))
-        pf = nxt
+        r, pf = epoch_with_prefetch(k, traces[k], pf)
+        results.append(r)
     if pf is not None:
         pf.result()
     wall = time.perf_counter() - t0

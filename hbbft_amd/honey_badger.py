@@ -351,7 +351,8 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
 
 
 def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
-              defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True):
+              defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True, preverify_at="first_drain",
+              after_prep=None):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
     ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
@@ -364,7 +365,11 @@ def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=Fals
     one batch (DeserializeCiphertext faults, epoch_state.rs:377-381) and every window of share
     messages in one batch before it is queued (hbbft_amd.wire).
     ``preverify``: the contributions' ciphertext checks and the first t + 1 + slack decryption shares
-    of each are checked on a second engine while the coin phase runs (_dec_preverify).
+    of each are checked on a second engine while the coin phase runs (_dec_preverify), started after
+    the coin phase's first drain (``preverify_at="first_drain"``) or with the epoch (``"start"``).
+    ``after_prep``: called (from a host-pool thread) once this epoch's host decryption prep is done --
+    a driver starts lower-priority host work there (the next epoch's coin prefetch) so that it does
+    not share the host threads with the prep.
     ``ba``: the coins come from Binary Agreement instances (``trace.with_ba``; default: when the
     trace has a BA side) -- hbbft_amd.binary_agreement's epochs, fixed coins and future-epoch queue,
     our SBV / Conf outcomes released along the message stream, coin combines deferred per window."""
@@ -375,7 +380,7 @@ def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=Fals
         sys.setswitchinterval(switch_interval)
     try:
         return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch,
-                          preverify)
+                          preverify, preverify_at, after_prep)
     finally:
         sys.setswitchinterval(old)
 
@@ -463,7 +468,9 @@ def _dec_preverify(engine2, keys, trace, prep, limit):
     Verdicts are pure, so checking them early changes no Step; the decrypt phase finds them in the
     cache and queues only the rest.  Returns the engine results for BatchVerifier._store (main
     thread)."""
+    t0 = time.perf_counter()
     huv_of, _ = prep.result()
+    t_prep = time.perf_counter() - t0
     pre = BatchVerifier(engine2)
     for p in sorted(trace.cts):
         if p in huv_of:
@@ -478,16 +485,23 @@ def _dec_preverify(engine2, keys, trace, prep, limit):
             continue
         cnt[p] = c + 1
         pre.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], huv_of[p], trace.cts[p][2])
-    return pre._run_jobs(pre._take_jobs())
+    t0 = time.perf_counter()
+    out = pre._run_jobs(pre._take_jobs())
+    return out, t_prep, time.perf_counter() - t0
 
 
 def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None,
-               preverify=True):
+               preverify=True, preverify_at="first_drain", after_prep=None):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     # the background host work leaves two of the host threads to the flows and the drain worker
     bg = threads if threads else max(1, hoststage.host_threads() - 2)
     prep = None if raw else _host_pool().submit(_decrypt_prep, trace.cts, keys.sks[our], bg)
+    if after_prep is not None:
+        if prep is None:
+            after_prep()
+        else:
+            prep.add_done_callback(lambda _f: after_prep())
     ver = BatchVerifier(engine, combine_engine(engine) if pipelined and hasattr(engine, "device") else None)
     ver.recording = defer                  # combines of the epoch run in one batch at the end
     pre_box = []  # the pre-verification future, once started
@@ -501,6 +515,8 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
         if _DEC_POOL is None:
             _DEC_POOL = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="hbh-pre")
         pre_box.append(_DEC_POOL.submit(_dec_preverify, combine_engine(engine), keys, trace, prep, limit))
+    if preverify_at == "start":
+        start_preverify()
     sk = keys.sks[our]
     n = keys.n
     t_all = time.perf_counter()
@@ -791,12 +807,18 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
     td = {p: ThresholdDecrypt(ni_dec, ver) for p in ps}
     if dec_pre is not None:  # the verdicts checked beside the coin phase (_dec_preverify) into the cache
         t1 = time.perf_counter()
-        pre = dec_pre.result()
-        ver.wait_s += time.perf_counter() - t1
+        pre, t_prep, t_eng = dec_pre.result()
+        res.timing["decrypt_pre_prep"], res.timing["decrypt_pre_engine"] = t_prep, t_eng
+        t2 = time.perf_counter()
+        ver.wait_s += t2 - t1
+        res.timing["decrypt_pre_wait"] = t2 - t1
         ver._store(pre)
+        res.timing["decrypt_pre_store"] = time.perf_counter() - t2
     for p in ps:
         ver.queue_ct(cts[p])  # (our own decryption share is not verified, threshold_decrypt.rs:167)
+    t1 = time.perf_counter()
     ver.drain()
+    res.timing["decrypt_drain"] = time.perf_counter() - t1
     res.timing["decrypt_setup"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     dec_out = {}
