@@ -488,6 +488,7 @@ class ThresholdSign:
         self.verifier = verifier
         self.doc_hash = None
         self.received_shares = {}  # node_id -> (idx, share); BTreeMap order = sorted ids
+        self.unverified = False    # a share was stored before the document was set (not checked)
         self.had_input = False
         self.terminated = False
 
@@ -536,11 +537,17 @@ class ThresholdSign:
             if pk is None or not self.verifier.sig_valid(pk, self.doc_hash, share):
                 return Step.fault(sender_id, "UnverifiedSignatureShareSender")
         self.received_shares[sender_id] = (idx, share if type(share) is bytes else bytes(share))
+        if self.doc_hash is None:
+            self.unverified = True
         if self.doc_hash is None or len(self.received_shares) <= ni.t:  # try_output's gate (:227-247)
             return Step()
         return self.try_output()
 
     def remove_invalid_shares(self):  # :200-213 -- the natural batch point: one drain
+        if self.doc_hash is not None and not self.unverified:
+            # every stored share passed is_share_valid when it arrived with the document set, and
+            # verdicts are pure: nothing to remove
+            return []
         for sid, (_, share) in self.received_shares.items():
             pk = self.netinfo.public_key_share(sid)
             if self.doc_hash is not None and pk is not None:
@@ -550,6 +557,8 @@ class ThresholdSign:
                   if not self.is_share_valid(sid, share)]
         for sid in faulty:
             del self.received_shares[sid]
+        if self.doc_hash is not None:
+            self.unverified = False
         return [Fault(sid, "UnverifiedSignatureShareSender") for sid in faulty]
 
     def is_share_valid(self, sender_id, share):  # :216-225
