@@ -859,8 +859,19 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
         return inst.handle_message(j, share)
 
     dec_msgs = [m for m in trace.dec_msgs if m[0] in td]  # (shares of a faulted contribution: no instance)
-    for p, out in _deliver(ver, dec_msgs, window, td,
-                           lambda p, j: ver.queue_dec(keys.pks[j], dec_sh[(p, j)], cts[p].huv, cts[p].w),
+    pks = keys.pks
+    ct_key = {p: (cts[p].huv, cts[p].w) for p in td}
+
+    def queue_dec(p, j):
+        # most shares were pre-verified (_dec_preverify): a cached verdict queues nothing
+        pk, sh, c = pks[j], dec_sh[(p, j)], ct_key[p]
+        if type(pk) is bytes and type(sh) is bytes:
+            d = dec_cache.get(c)
+            if d is not None and (pk, sh) in d:
+                return
+        ver.queue_dec(pk, sh, c[0], c[1])
+
+    for p, out in _deliver(ver, dec_msgs, window, td, queue_dec,
                            hand_dec, res, "dec", pipelined, limit,
                            _decoder(engine, trace.raw_dec, dec_sh, wire.decode_dec_share_msgs) if raw else None):
         dec_out[p] = out
