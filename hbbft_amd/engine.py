@@ -50,7 +50,10 @@ def _join(points, size):
     if isinstance(points, (bytes, bytearray)):
         b = bytes(points)
     else:
-        b = b"".join(bytes(p) for p in points)
+        try:  # bytes-like items (bytes, bytearray, memoryview, uint8 arrays) join directly
+            b = b"".join(points)
+        except TypeError:
+            b = b"".join(bytes(p) for p in points)
     if len(b) % size:
         raise ValueError("point buffer length %d is not a multiple of %d" % (len(b), size))
     return b
