@@ -486,8 +486,35 @@ def _dec_preverify(engine2, keys, trace, prep, limit):
         cnt[p] = c + 1
         pre.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], huv_of[p], trace.cts[p][2])
     t0 = time.perf_counter()
-    out = pre._run_jobs(pre._take_jobs())
+    out = _one_call(engine2, pre._take_jobs())
     return out, t_prep, time.perf_counter() - t0
+
+
+def _one_call(engine2, jobs):
+    """The pre-verification's ciphertext and decryption-share checks in ONE engine call: Ciphertext::verify
+    e(U, H_uv) == e(g1, W) has the shape of a share check e(share, H_uv) == e(pk, W) with share = U and
+    pk = g1, so the ciphertexts ride along as extra rows of verify_dec_shares over the same (H_uv, W)
+    table (the same pairing equation as hbh_verify_ciphertexts, sides swapped).  Returns the
+    BatchVerifier._store results of both kinds."""
+    by = {kind: (keys, args) for kind, keys, args in jobs}
+    if set(by) != {"ct", "dec"}:
+        return BatchVerifier(engine2)._run_jobs(jobs)
+    ckeys, _ = by["ct"]
+    dkeys, (shares, pks, huvt, wt, cidx) = by["dec"]
+    shares, pks, huvt, wt, cidx = list(shares), list(pks), list(huvt), list(wt), list(cidx)
+    ctab = {c: i for i, c in enumerate(zip(huvt, wt))}
+    for u, w, h in ckeys:  # ct keys: (U, W, H_uv)
+        c = ctab.get((h, w))
+        if c is None:
+            c = ctab[(h, w)] = len(huvt)
+            huvt.append(h)
+            wt.append(w)
+        shares.append(u)
+        pks.append(G1_GEN)
+        cidx.append(c)
+    v = engine2.verify_dec_shares(shares, pks, huvt, wt, cidx)
+    nd = len(dkeys)
+    return [("dec", dkeys, v[:nd]), ("ct", ckeys, v[nd:])]
 
 
 def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None,

@@ -200,3 +200,32 @@ def test_epoch_coins_through_binary_agreement(engine, n, extra):
         assert (kind, p, flt.node_id) in (trace.bad | ba.bad), (kind, p, flt)
     one = run_epoch(engine, keys, trace, window=1, pipelined=False)
     assert (one.ba_decisions, one.ba_coins, one.plaintexts) == (res.ba_decisions, res.ba_coins, res.plaintexts)
+
+
+def test_preverify_one_call_matches_separate_calls(engine):
+    """honey_badger._one_call: the ciphertext checks ride as extra rows of the decryption-share call
+    (e(U, H) == e(g1, W) in share-check form); the verdicts equal verify_ciphertexts' and
+    verify_dec_shares' separate calls, incl. a ciphertext with another contribution's W, one with
+    another contribution's U, and forged shares."""
+    from hbbft_amd import hoststage
+    from hbbft_amd.honey_badger import _one_call
+    from hbbft_amd.protocol import BatchVerifier, Ciphertext
+    rng = random.Random(77)
+    keys = NetworkKeys(engine, 7, 2, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=1, bad_every=3, proposal_bytes=64)
+    ps = sorted(trace.cts)
+    cts = {p: list(trace.cts[p]) for p in ps}
+    cts[ps[0]][2] = cts[ps[1]][2]               # W of another contribution
+    cts[ps[2]][0] = cts[ps[3]][0]               # U of another contribution
+    huv = hoststage.hash_g1_g2([cts[p][0] for p in ps], [cts[p][1] for p in ps])
+    pre = BatchVerifier(engine)
+    for p, h in zip(ps, huv):
+        pre.queue_ct(Ciphertext(cts[p][0], cts[p][1], cts[p][2], h))
+    for p, j in trace.dec_msgs:
+        c = ps.index(p)
+        pre.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], huv[c], cts[p][2])
+    jobs = pre._take_jobs()
+    merged = {kind: (keys_, v) for kind, keys_, v in _one_call(engine, jobs)}
+    separate = {kind: (keys_, v) for kind, keys_, v in BatchVerifier(engine)._run_jobs(jobs)}
+    assert merged == separate
+    assert 0 < sum(separate["ct"][1]) < len(ps) and 0 < sum(separate["dec"][1]) < len(separate["dec"][0])

@@ -81,6 +81,9 @@ def teach(eng, keys, tr):
         eng.u_of_share[bytes(s)] = tr.cts[p][0]
         if ("dec", p, j) not in bad:
             eng.valid.add((bytes(keys.pks[j]), bytes(s)))
+    from hbbft_amd.sync_key_gen import G1_GEN
+    for p in tr.cts:  # a ciphertext check as a share-check row (honey_badger._one_call): (g1, U)
+        eng.valid.add((bytes(G1_GEN), bytes(tr.cts[p][0])))
     for (p, e, j), s in tr.ba.shares.items():
         if ("coin", p, j) not in bad:
             eng.valid.add((bytes(keys.pks[j]), bytes(s)))
