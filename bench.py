@@ -559,9 +559,9 @@ def main():
                                 if args.impl in ("pair", "auto", "quad", "oct") else None)
         kernels = [main_k]
         if prep_n:
-            kernels.append(roofline_entry("hbs::k_pair_prep" if args.impl in ("pair", "auto", "quad", "oct") else "hb::k_g2_prepare",
+            kernels.append(roofline_entry("hbs::k_oct_prep" if args.impl in ("pair", "auto", "quad", "oct") else "hb::k_g2_prepare",
                                           prep_n, prep_ms / prep_n, nh, workcount.PAIR_PREP_DOC, "document (G2 walk)",
-                                          nh * 4 / 64 / 1024))  # one lane quad per point
+                                          nh * 8 / 64 / 1024))  # one lane octo per point
         out = {
             "metric": METRIC, "value": value, "unit": "shares/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
@@ -704,9 +704,9 @@ def run_decrypt(args, eng, world, rank, dev):
                                 workcount.PAIR_CHECK_TABLE, "decryption-share check", pair_waves_per_simd(n))
         kernels = [main_k]
         if prep_n:
-            kernels.append(roofline_entry("hbs::k_pair_prep", prep_n, prep_ms / prep_n, 2 * len(mine),
+            kernels.append(roofline_entry("hbs::k_oct_prep", prep_n, prep_ms / prep_n, 2 * len(mine),
                                           workcount.PAIR_PREP_DOC, "G2 point (H_uv, W) walk",
-                                          2 * len(mine) * 4 / 64 / 1024))  # one lane quad per point
+                                          2 * len(mine) * 8 / 64 / 1024))  # one lane octo per point
         line = {
             "metric": "verified decryption shares/sec (whole node), N=64 f=21", "value": total / (ms_step / 1e3),
             "unit": "shares/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,

@@ -230,7 +230,7 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
     HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
     HBH_CHECK(inf[k]->ensure(sd[k].nq));
     hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
-    HBH_CHECK(hbl::pair_prep(s, (int)sd[k].nq, sd[k].q, tab[k]->p, (uint8_t*)inf[k]->p));
+    HBH_CHECK(hbl::oct_prep(s, (int)sd[k].nq, sd[k].q, tab[k]->p, (uint8_t*)inf[k]->p));
     e->timer.end(s, t);
     sd[k].lines = tab[k]->p;
     sd[k].qinf = (const uint8_t*)inf[k]->p;

@@ -26,6 +26,8 @@ struct PairSideDesc {
 };
 size_t pair_table_bytes(size_t nq);
 hipError_t pair_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* qinf);
+// the same tables from lane octos (k_oct_prep.hip: eight lanes per point)
+hipError_t oct_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* qinf);
 // flags: bit 0 negates P2 (pairing equality), bit 1 conjugates f (single pairing value, with
 // value_out: e(P1,Q1)^3 e(P2,Q2)^3 as 144 canonical words per check)
 hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,

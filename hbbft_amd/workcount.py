@@ -77,7 +77,7 @@ def mads(fpmul, fpsqr=0):
 # per-unit algorithmic work of each kernel: (Fp ops, of which Fp squarings)
 PAIR_CHECK_WALK = (MILLER_2PAIR + G2_WALK + FINAL_EXP, FP_INV_SQR)   # k_pair_verify, one side walked
 PAIR_CHECK_TABLE = (MILLER_2PAIR + FINAL_EXP, FP_INV_SQR)            # k_pair_verify, both sides tabled
-PAIR_PREP_DOC = (G2_WALK, 0)                                         # k_pair_prep, per G2 point
+PAIR_PREP_DOC = (G2_WALK, 0)                                         # k_oct_prep (k_pair_prep), per G2 point
 REFERENCE_CHECK_OPS = (REFERENCE_CHECK, FP_INV_SQR)                  # two separate pairings
 
 G1_DBL = (7, 5)

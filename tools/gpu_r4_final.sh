@@ -2,7 +2,7 @@
 # round 4 closing evidence (one fresh box): GPU suite, smoke, the four bench lines (default sign line
 # = the driver's BENCH), the default bench under rocprofv3 --kernel-trace --stats, separate PMC passes
 # (FETCH_SIZE / WRITE_SIZE / SQ counters) per workload for profiles/r04/pmc_traffic.json, and a
-# two-stream kernel trace of the sign line (k_pair_prep overlap).  Every GPU step has its own limit.
+# two-stream kernel trace of the sign line (line-table prep overlap).  Every GPU step has its own limit.
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT

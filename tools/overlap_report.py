@@ -14,7 +14,7 @@ for f in files:
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0], r.get("Queue_Id")))
 rows.sort()
 pair = [(s, e, q) for s, e, n, q in rows if "k_pair_verify" in n]
-prep = [(s, e, q) for s, e, n, q in rows if "k_pair_prep" in n]
+prep = [(s, e, q) for s, e, n, q in rows if ("k_pair_prep" in n or "k_oct_prep" in n)]
 tot = hidden = 0
 for s, e, q in prep:
     d = e - s
