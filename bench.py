@@ -69,11 +69,17 @@ def log(*a):
 
 
 def dist_backend():
-    """nccl (= RCCL) by default; HBH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks then
-    share devices round-robin and the timing reduction runs on host tensors).  Decided from the
-    device COUNT, which does not initialise the GPU runtime (a parent that spawns the ranks must
-    not)."""
-    return os.environ.get("HBH_DIST_BACKEND", "nccl" if torch.cuda.device_count() > 0 else "gloo")
+    """gloo on host tensors by default: the ranks exchange only a barrier, the max step time and
+    per-rank reports, and the design has no device collective (north star: RCCL is
+    deliberately unused), so a multi-GPU record carries no RCCL traffic.  HBH_DIST_BACKEND=nccl
+    selects RCCL for the same few host values (moved to the device); HBH_REHEARSE=1 (or the legacy
+    HBH_DIST_BACKEND=gloo) rehearses N ranks on fewer GPUs (ranks share devices round-robin)."""
+    return os.environ.get("HBH_DIST_BACKEND", "gloo")
+
+
+def rehearsal():
+    """N ranks on fewer devices than N (tests/test_bench_launch.py): explicit opt-in only."""
+    return os.environ.get("HBH_REHEARSE") == "1" or os.environ.get("HBH_DIST_BACKEND") == "gloo"
 
 
 def _free_port():
@@ -106,8 +112,8 @@ def launch(args):
       * --launcher pool: one process drives the in-ABI engine pool over N devices;
     fewer visible devices than asked for is an error (exit 2), never a silent 1-GPU run."""
     visible = torch.cuda.device_count()
-    # HBH_DIST_BACKEND=gloo explicitly: rehearse N ranks sharing the visible device(s)
-    need = 1 if os.environ.get("HBH_DIST_BACKEND") == "gloo" else args.gpus
+    # rehearsal (HBH_REHEARSE=1 or HBH_DIST_BACKEND=gloo explicitly): N ranks share the visible device(s)
+    need = 1 if rehearsal() else args.gpus
     env = os.environ.get("WORLD_SIZE")
     if env is not None:
         if int(env) != args.gpus:

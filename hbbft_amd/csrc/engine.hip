@@ -217,7 +217,7 @@ hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, con
 }
 
 // HBH_IMPL_PAIR: a G2 side shared through an index map by at least 4 checks per point gets a line
-// table (k_pair_prep); every other side is walked inside the verify kernel.
+// table (k_oct_prep); every other side is walked inside the verify kernel.
 int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_p1, const void* d_q1, size_t nq1,
                 const uint32_t* d_i1, const void* d_p2, const void* d_q2, size_t nq2, const uint32_t* d_i2, int flags,
                 uint8_t* d_v, uint32_t* d_value, int slot) {
@@ -225,7 +225,7 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
   DevBuf* tab[2] = {&e->ptab[slot][0], &e->ptab[slot][1]};
   DevBuf* inf[2] = {&e->pinf[slot][0], &e->pinf[slot][1]};
   for (int k = 0; k < 2; k++) {
-    // WAVE walks every side: a table costs a serial 68-step walk (k_pair_prep) before the first check
+    // WAVE walks every side: a table costs a serial 68-step walk (k_oct_prep) before the first check
     if (!sd[k].idx || sd[k].nq * 4 > n || impl == HBH_IMPL_WAVE) continue;
     HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
     HBH_CHECK(inf[k]->ensure(sd[k].nq));

@@ -33,6 +33,11 @@
 namespace hh {
 
 // ---------------------------------------------------------------- constants
+static Fq fq_from_canon_raw(const uint64_t* v, const Fq& r2) {
+  Fq a;
+  memcpy(a.l, v, sizeof(a.l));
+  return fq_mul(a, r2);
+}
 static Consts make_consts() {
   Consts c;
   // R mod p = 2^384 mod p by modular doubling of 1; R^2 mod p = R * 2^384 mod p likewise
@@ -50,6 +55,12 @@ static Consts make_consts() {
   memcpy(c.r2.l, v, sizeof(v));
   const uint64_t four[6] = {4, 0, 0, 0, 0, 0};
   c.b1 = fq_mul(*(const Fq*)four, c.r2);
+  // 1/2 = (p + 1) / 2
+  uint64_t half[6];
+  memcpy(half, P, sizeof(P));
+  half[0] += 1;  // p is odd: no carry
+  for (int i = 0; i < 6; i++) half[i] = (half[i] >> 1) | (i < 5 ? half[i + 1] << 63 : 0);
+  c.inv2 = fq_from_canon_raw(half, c.r2);
   // p - 2, (p - 3) / 4, (p - 1) / 2
   memcpy(c.pm2, P, sizeof(P));
   c.pm2[0] -= 2;
@@ -68,27 +79,42 @@ const Consts& consts() {
   return c;
 }
 
+// Square root in Fq2 by the norm (p = 3 mod 4, u^2 = -1): with s = v^((p-3)/4), s v is a root of v and
+// s^2 v = v^((p-1)/2) its Legendre symbol, so each Fq exponentiation decides and extracts at once.
+// a = a0 + a1 u is a square iff its norm a0^2 + a1^2 is; then x0^2 = delta = (a0 +- sqrt(norm)) / 2
+// (exactly one sign is a square) and x1 = a1 / (2 x0) = a1 t / 2 with t = delta^((p-3)/4) = 1 / x0.
+// Two or three Fq exponentiations instead of two Fq2 ones (the previous algorithm); which of the
+// two roots comes out does not matter: G2::rand keeps the one its `greatest` bit selects.
 bool f2_sqrt(const Fq2& a, Fq2& out) {
-  if (f2_is_zero(a)) {
-    out = a;
-    return true;
-  }
   const Consts& k = consts();
-  const Fq2 a1 = f2_pow(a, k.pm3d4, 6);
-  const Fq2 alpha = f2_mul(f2_sqr(a1), a);
-  const Fq2 a0 = f2_mul(f2_conj(alpha), alpha);  // alpha^p alpha
-  const Fq2 minus_one = {fq_neg(fq_one()), fq_zero()};
-  if (f2_eq(a0, minus_one)) return false;
-  const Fq2 x0 = f2_mul(a1, a);
-  Fq2 r;
-  if (f2_eq(alpha, minus_one)) {
-    r = {fq_neg(x0.c1), x0.c0};  // x0 * u
+  const Fq one = fq_one();
+  if (fq_is_zero(a.c1)) {
+    if (fq_is_zero(a.c0)) {
+      out = a;
+      return true;
+    }
+    const Fq s = fq_pow(a.c0, k.pm3d4, 6);
+    const Fq root = fq_mul(s, a.c0);
+    if (fq_eq(fq_mul(root, s), one))
+      out = {root, fq_zero()};
+    else
+      out = {fq_zero(), root};  // root^2 = -a0, so (root u)^2 = a0
   } else {
-    r = f2_mul(f2_pow(f2_add(f2_one(), alpha), k.pm1d2, 6), x0);
+    const Fq norm = fq_add(fq_sqr(a.c0), fq_sqr(a.c1));
+    const Fq s = fq_pow(norm, k.pm3d4, 6);
+    const Fq gamma = fq_mul(s, norm);
+    if (!fq_eq(fq_mul(gamma, s), one)) return false;  // the norm is not a square
+    Fq delta = fq_mul(fq_add(a.c0, gamma), k.inv2);
+    Fq t = fq_pow(delta, k.pm3d4, 6);
+    Fq x0 = fq_mul(t, delta);
+    if (!fq_eq(fq_mul(x0, t), one)) {
+      delta = fq_mul(fq_sub(a.c0, gamma), k.inv2);
+      t = fq_pow(delta, k.pm3d4, 6);
+      x0 = fq_mul(t, delta);
+    }
+    out = {x0, fq_mul(fq_mul(a.c1, t), k.inv2)};
   }
-  if (!f2_eq(f2_sqr(r), a)) return false;
-  out = r;
-  return true;
+  return f2_eq(f2_sqr(out), a);
 }
 
 // ---------------------------------------------------------------- encodings
@@ -111,6 +137,24 @@ void g2_to_abi(const Jac<Fq2>& p, uint8_t* out) {
   fq_to_le(x.c1, out + 48);
   fq_to_le(y.c0, out + 96);
   fq_to_le(y.c1, out + 144);
+}
+void g1_aff_to_abi(const Aff<Fq>& p, uint8_t* out) {
+  if (p.inf) {
+    memset(out, 0, HBH_G1_BYTES);
+    return;
+  }
+  fq_to_le(p.x, out);
+  fq_to_le(p.y, out + 48);
+}
+void g2_aff_to_abi(const Aff<Fq2>& p, uint8_t* out) {
+  if (p.inf) {
+    memset(out, 0, HBH_G2_BYTES);
+    return;
+  }
+  fq_to_le(p.x.c0, out);
+  fq_to_le(p.x.c1, out + 48);
+  fq_to_le(p.y.c0, out + 96);
+  fq_to_le(p.y.c1, out + 144);
 }
 static bool all_zero(const uint8_t* b, size_t n) {
   for (size_t i = 0; i < n; i++)
@@ -275,12 +319,277 @@ struct ChaChaRng {
   bool gen_bool() { return (next_u32() & 1) == 1; }
 };
 
-// ---------------------------------------------------------------- hash to G2
-static const uint64_t H2_LIMBS[8] = {0xcf1c38e31c7238e5ull, 0x1616ec6e786f0c70ull, 0x21537e293a6691aeull,
-                                     0xa628f1cb4d9e82efull, 0xa68a205b2e5a7ddfull, 0xcd91de4547085abaull,
-                                     0x091d50792876a202ull, 0x05d543a95414e7f1ull};
+// ---------------------------------------------------------------- scalars (Fr, little-endian 64-bit limbs)
+static const uint64_t R_ORDER[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                                    0x73eda753299d7d48ull};
+static bool geq_r(const uint64_t* a) {
+  for (int i = 3; i >= 0; i--)
+    if (a[i] != R_ORDER[i]) return a[i] > R_ORDER[i];
+  return true;
+}
+static void sub_r(uint64_t* a) {
+  uint64_t br = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 d = (u128)a[i] - R_ORDER[i] - br;
+    a[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+}
+// k mod r for any 256-bit k (k < 2^256 < 3 r): the group elements are of order r, so every scalar
+// multiplication below is by the reduced scalar
+static void reduce_r(uint64_t* k) {
+  while (geq_r(k)) sub_r(k);
+}
+// a b mod r (a, b < r): Montgomery CIOS with R = 2^256, then one more product by R^2 mod r
+static void fr_mont(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+  const uint64_t RINV = 0xfffffffeffffffffull;  // -r^-1 mod 2^64
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < 4; j++) {
+      const u128 s = (u128)a[j] * b[i] + t[j] + c;
+      t[j] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    u128 s = (u128)t[4] + c;
+    t[4] = (uint64_t)s;
+    t[5] = (uint64_t)(s >> 64);
+    const uint64_t m = t[0] * RINV;
+    s = (u128)m * R_ORDER[0] + t[0];
+    c = (uint64_t)(s >> 64);
+    for (int j = 1; j < 4; j++) {
+      s = (u128)m * R_ORDER[j] + t[j] + c;
+      t[j - 1] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    s = (u128)t[4] + c;
+    t[3] = (uint64_t)s;
+    t[4] = t[5] + (uint64_t)(s >> 64);
+  }
+  memcpy(out, t, 32);
+  if (t[4] || geq_r(out)) sub_r(out);
+}
+static void fr_mul(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+  static const uint64_t R2R[4] = {0xc999e990f3f29c6dull, 0x2b6cedcb87925c23ull, 0x05d314967254398full,
+                                  0x0748d9d99f59ff11ull};  // 2^512 mod r
+  uint64_t t[4];
+  fr_mont(a, b, t);
+  fr_mont(t, R2R, out);
+}
+// k = q d + rem for a 64-bit d: k becomes q, returns rem
+static uint64_t divmod_u64(uint64_t* k, int nl, uint64_t d) {
+  u128 rem = 0;
+  for (int i = nl - 1; i >= 0; i--) {
+    const u128 cur = (rem << 64) | k[i];
+    k[i] = (uint64_t)(cur / d);
+    rem = cur % d;
+  }
+  return (uint64_t)rem;
+}
+// width-5 NAF of a non-negative integer (nl <= 2 little-endian limbs): digits in {0, +-1, ..., +-15},
+// at most 64 nl + 1 of them, least significant first; returns the digit count
+static int wnaf5(const uint64_t* a, int nl, int8_t* out) {
+  uint64_t k[3] = {0, 0, 0};
+  memcpy(k, a, 8 * (size_t)nl);
+  int n = 0;
+  while (k[0] | k[1] | k[2]) {
+    int d = 0;
+    if (k[0] & 1) {
+      d = (int)(k[0] & 31);
+      if (d >= 16) d -= 32;
+      // k -= d
+      if (d > 0) {
+        const u128 s = (u128)k[0] - (uint64_t)d;
+        k[0] = (uint64_t)s;
+        uint64_t br = (uint64_t)(s >> 64) & 1;
+        for (int i = 1; i < 3 && br; i++) br = (k[i]-- == 0);
+      } else {
+        const u128 s = (u128)k[0] + (uint64_t)(-d);
+        k[0] = (uint64_t)s;
+        uint64_t c = (uint64_t)(s >> 64);
+        for (int i = 1; i < 3 && c; i++) c = (++k[i] == 0);
+      }
+    }
+    out[n++] = (int8_t)d;
+    k[0] = (k[0] >> 1) | (k[1] << 63);
+    k[1] = (k[1] >> 1) | (k[2] << 63);
+    k[2] >>= 1;
+  }
+  return n;
+}
+// sum_i [digit_i] base_i for M bases with width-5 NAF digits, one doubling chain; tab[i][j] = (2 j + 1) base_i
+template <class F, int M>
+static Jac<F> multi_wnaf(const Jac<F> (*tab)[8], int8_t (*naf)[130], const int* len) {
+  int top = 0;
+  for (int i = 0; i < M; i++) top = std::max(top, len[i]);
+  Jac<F> r = jac_inf<F>();
+  for (int b = top - 1; b >= 0; b--) {
+    r = jac_dbl(r);
+    for (int i = 0; i < M; i++) {
+      if (b >= len[i] || !naf[i][b]) continue;
+      const int d = naf[i][b];
+      r = jac_add(r, d > 0 ? tab[i][d >> 1] : jac_neg(tab[i][(-d) >> 1]));
+    }
+  }
+  return r;
+}
+template <class F>
+static void odd_multiples(const Jac<F>& p, Jac<F>* t8) {
+  t8[0] = p;
+  const Jac<F> p2 = jac_dbl(p);
+  for (int j = 1; j < 8; j++) t8[j] = jac_add(t8[j - 1], p2);
+}
 
-static Jac<Fq2> g2_rand(ChaChaRng& rng) {
+// ---------------------------------------------------------------- endomorphisms
+// G1: phi(x, y) = (beta x, y) acts as [lambda] on G1, lambda = z^2 - 1 (z = -0xd201000000010000), and
+// r = lambda^2 + lambda + 1, so k = k2 lambda + k1 with k1, k2 < 2^128 (GLV).
+static const uint64_t BETA_CANON[6] = {0x8bfd00000000aaacull, 0x409427eb4f49fffdull, 0x897d29650fb85f9bull,
+                                       0xaa0d857d89759ad4ull, 0xec02408663d4de85ull, 0x1a0111ea397fe699ull};
+static const u128 LAMBDA = ((u128)0xac45a4010001a402ull << 64) | 0x00000000ffffffffull;
+// G2: psi(x, y) = (conj(x) cx, conj(y) cy) (untwist-Frobenius-twist) on all of E'(Fq2); on G2 it acts
+// as [p] = [z] mod r.  cx = CX1 u.
+static const uint64_t CX1_CANON[6] = {0x8bfd00000000aaadull, 0x409427eb4f49fffdull, 0x897d29650fb85f9bull,
+                                      0xaa0d857d89759ad4ull, 0xec02408663d4de85ull, 0x1a0111ea397fe699ull};
+static const uint64_t CY_CANON[2][6] = {
+    {0xf1ee7b04121bdea2ull, 0x304466cf3e67fa0aull, 0xef396489f61eb45eull, 0x1c3dedd930b1cf60ull,
+     0xe2e9c448d77a2cd9ull, 0x135203e60180a68eull},
+    {0xc81084fbede3cc09ull, 0xee67992f72ec05f4ull, 0x77f76e17009241c5ull, 0x48395dabc2d3435eull,
+     0x6831e36d6bd17ffeull, 0x06af0e0437ff400bull}};
+static const uint64_t Z_ABS = 0xd201000000010000ull;
+// h2 P = [KCOF] Q_bp for every P on E'(Fq2), Q_bp the Budroni-Pintore image below (KCOF = h2 s^-1 mod r,
+// s = (z^2 - z - 1) + (z - 1) p + 2 p^2 mod r, the scalar by which Q_bp's map acts on G2)
+static const uint64_t KCOF[4] = {0x55555554aaaaaaabull, 0x37d2aaab55543d54ull, 0x66689d580335f2acull,
+                                 0x26a48d1bb889d46dull};
+struct EndoConsts {
+  Fq beta, cx1;
+  Fq2 cy;
+};
+static const EndoConsts& endo() {
+  static const EndoConsts e = [] {
+    EndoConsts c;
+    c.beta = fq_from_canon(BETA_CANON);
+    c.cx1 = fq_from_canon(CX1_CANON);
+    c.cy = {fq_from_canon(CY_CANON[0]), fq_from_canon(CY_CANON[1])};
+    return c;
+  }();
+  return e;
+}
+static Jac<Fq2> psi(const Jac<Fq2>& p) {
+  const EndoConsts& e = endo();
+  const Fq2 x = f2_conj(p.x);
+  return {{fq_neg(fq_mul(x.c1, e.cx1)), fq_mul(x.c0, e.cx1)}, f2_mul(f2_conj(p.y), e.cy), f2_conj(p.z)};
+}
+static Jac<Fq> phi(const Jac<Fq>& p) { return {fq_mul(p.x, endo().beta), p.y, p.z}; }
+template <class F>
+static Jac<F> mul_zabs(const Jac<F>& p) {
+  Jac<F> r = p;
+  for (int b = 62; b >= 0; b--) {
+    r = jac_dbl(r);
+    if ((Z_ABS >> b) & 1) r = jac_add(r, p);
+  }
+  return r;
+}
+
+// [k] P for P in G1 (subgroup contract): GLV split, width-5 NAF, 129 doublings
+static Jac<Fq> g1_mul_glv(const Jac<Fq>& p, const uint64_t* k_in) {
+  uint64_t k[4];
+  memcpy(k, k_in, 32);
+  reduce_r(k);
+  // k = q lambda + rem by shift-subtract (lambda > 2^127: track the bit shifted out of rem)
+  u128 rem = 0, q = 0;
+  for (int b = 255; b >= 0; b--) {
+    const bool carry = (rem >> 127) != 0;
+    rem = (rem << 1) | ((k[b >> 6] >> (b & 63)) & 1);
+    if (carry || rem >= LAMBDA) {
+      rem -= LAMBDA;
+      q |= (u128)1 << b;  // q < 2^128: b < 128 whenever this fires
+    }
+  }
+  const uint64_t k1[2] = {(uint64_t)rem, (uint64_t)(rem >> 64)};
+  const uint64_t k2[2] = {(uint64_t)q, (uint64_t)(q >> 64)};
+  Jac<Fq> tab[2][8];
+  odd_multiples(p, tab[0]);
+  for (int j = 0; j < 8; j++) tab[1][j] = phi(tab[0][j]);
+  int8_t naf[2][130];
+  const int len[2] = {wnaf5(k1, 2, naf[0]), wnaf5(k2, 2, naf[1])};
+  return multi_wnaf<Fq, 2>(tab, naf, len);
+}
+
+// [k] Q for Q in G2 (subgroup contract): k mod r in base |z| (four digits < 2^64), [|z|] = -psi on G2,
+// so k Q = sum_i d_i (-psi)^i (Q); width-5 NAF per digit, 65 doublings
+static Jac<Fq2> g2_mul_gls(const Jac<Fq2>& q, const uint64_t* k_in) {
+  uint64_t k[4];
+  memcpy(k, k_in, 32);
+  reduce_r(k);
+  uint64_t d[4];
+  for (int i = 0; i < 3; i++) d[i] = divmod_u64(k, 4, Z_ABS);
+  d[3] = k[0];  // k < r < |z|^4: the last quotient fits one limb
+  Jac<Fq2> tab[4][8];
+  odd_multiples(q, tab[0]);
+  for (int i = 1; i < 4; i++)
+    for (int j = 0; j < 8; j++) tab[i][j] = jac_neg(psi(tab[i - 1][j]));
+  int8_t naf[4][130];
+  int len[4];
+  for (int i = 0; i < 4; i++) len[i] = wnaf5(&d[i], 1, naf[i]);
+  return multi_wnaf<Fq2, 4>(tab, naf, len);
+}
+
+// Q_bp = [z^2 - z - 1] P + [z - 1] psi(P) + psi^2(2P) for any P on E'(Fq2) (Budroni-Pintore 2017, the
+// chain of the IETF hash-to-curve clear_cofactor): Q_bp lies in G2 and h2 P = [KCOF] Q_bp, so pairing
+// 0.14's cofactor multiplication by the 636-bit h2 becomes two 64-bit chains by |z| plus a GLS
+// multiplication (or none at all when the caller multiplies by a scalar anyway: W = H r).
+static Jac<Fq2> cofactor_bp(const Jac<Fq2>& p) {
+  const Jac<Fq2> t1 = jac_neg(mul_zabs(p));  // [z] P
+  Jac<Fq2> t2 = psi(p);
+  Jac<Fq2> t3 = psi(psi(jac_dbl(p)));
+  t3 = jac_add(t3, jac_neg(t2));
+  t2 = jac_add(t1, t2);
+  t2 = jac_neg(mul_zabs(t2));  // [z] ([z] P + psi(P))
+  t3 = jac_add(t3, t2);
+  t3 = jac_add(t3, jac_neg(t1));
+  return jac_add(t3, jac_neg(p));
+}
+
+// fixed-base comb of g1 (encrypt_with_rng's U = g1 r): T[w][d - 1] = d 2^(8 w) g1 (affine), 32 x 255 points
+// built once per process; [k] g1 = sum_w T[w][byte_w(k)]: 32 mixed additions, no doubling
+static const uint64_t G1_CANON[12] = {0xfb3af00adb22c6bbull, 0x6c55e83ff97a1aefull, 0xa14e3a3f171bac58ull,
+                                      0xc3688c4f9774b905ull, 0x2695638c4fa9ac0full, 0x17f1d3a73197d794ull,
+                                      0x0caa232946c5e7e1ull, 0xd03cc744a2888ae4ull, 0x00db18cb2c04b3edull,
+                                      0xfcf5e095d5d00af6ull, 0xa09e30ed741d8ae4ull, 0x08b3f481e3aaa0f1ull};
+static const std::vector<Aff<Fq>>& g1_comb() {
+  static const std::vector<Aff<Fq>> tab = [] {
+    std::vector<Aff<Fq>> t(32 * 255);
+    Aff<Fq> base = {fq_from_canon(G1_CANON), fq_from_canon(G1_CANON + 6), false};
+    std::vector<Jac<Fq>> row(256);
+    for (int w = 0; w < 32; w++) {
+      row[0] = jac_from_aff(base);
+      for (int d = 1; d < 256; d++) row[d] = jac_add_aff(row[d - 1], base.x, base.y);  // row[d] = (d+1) base
+      std::vector<Aff<Fq>> aff(256);
+      jac_batch_affine(row.data(), aff.data(), 256);
+      for (int d = 0; d < 255; d++) t[w * 255 + d] = aff[d];
+      base = aff[255];  // 256 base
+    }
+    return t;
+  }();
+  return tab;
+}
+static Jac<Fq> g1_mul_gen(const uint64_t* k_in) {
+  uint64_t k[4];
+  memcpy(k, k_in, 32);
+  reduce_r(k);
+  const std::vector<Aff<Fq>>& t = g1_comb();
+  Jac<Fq> r = jac_inf<Fq>();
+  for (int w = 0; w < 32; w++) {
+    const int d = (int)((k[w >> 3] >> (8 * (w & 7))) & 0xff);
+    if (d) r = jac_add_aff(r, t[w * 255 + d - 1].x, t[w * 255 + d - 1].y);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- hash to G2
+// pairing 0.14 G2::rand up to the cofactor multiplication: the first sampled curve point (x, y) whose
+// h2 multiple is not O, returned as Q_bp (h2 (x, y) = [KCOF] Q_bp; Q_bp = O exactly when h2 (x, y) = O)
+static Jac<Fq2> g2_rand_bp(ChaChaRng& rng) {
   const Fq four = consts().b1;
   const Fq2 b2 = {four, four};  // 4 (1 + u)
   for (;;) {
@@ -293,19 +602,25 @@ static Jac<Fq2> g2_rand(ChaChaRng& rng) {
     const Fq2 ny = f2_neg(y);
     // keep y iff (y > -y) == greatest
     if (f2_gt(y, ny) != greatest) y = ny;
-    const Jac<Fq2> p = jac_mul(Jac<Fq2>{x, y, f2_one()}, H2_LIMBS, 8);
-    if (!f2_is_zero(p.z)) return p;
+    const Jac<Fq2> q = cofactor_bp(Jac<Fq2>{x, y, f2_one()});
+    if (!f2_is_zero(q.z)) return q;
   }
 }
 
-static void hash_g2(const uint8_t* msg, size_t len, uint8_t* out) {
+// Q_bp of hash_g2(msg)
+static Jac<Fq2> hash_g2_bp(const uint8_t* msg, size_t len) {
   uint8_t seed[32];
   sha3_256(msg, len, seed);
   ChaChaRng rng(seed);
-  g2_to_abi(g2_rand(rng), out);
+  return g2_rand_bp(rng);
 }
 
-static void hash_g1_g2(const uint8_t* u_abi, const uint8_t* v, size_t vlen, uint8_t* out) {
+static void hash_g2(const uint8_t* msg, size_t len, uint8_t* out) {
+  g2_to_abi(g2_mul_gls(hash_g2_bp(msg, len), KCOF), out);
+}
+
+// the message hash_g1_g2 hashes: (V if |V| <= 64 else sha3(V)) || compress(U)
+static std::vector<uint8_t> g1_g2_msg(const uint8_t* u_abi, const uint8_t* v, size_t vlen) {
   std::vector<uint8_t> m;
   if (vlen > 64) {
     m.resize(32);
@@ -316,6 +631,11 @@ static void hash_g1_g2(const uint8_t* u_abi, const uint8_t* v, size_t vlen, uint
   uint8_t cu[48];
   g1_compress(u_abi, cu);
   m.insert(m.end(), cu, cu + 48);
+  return m;
+}
+
+static void hash_g1_g2(const uint8_t* u_abi, const uint8_t* v, size_t vlen, uint8_t* out) {
+  const std::vector<uint8_t> m = g1_g2_msg(u_abi, v, vlen);
   hash_g2(m.data(), m.size(), out);
 }
 
@@ -472,7 +792,7 @@ int hbh_host_g1_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_
     }
     uint64_t k[4];
     scalar_limbs(scalars + i * 32, k);
-    hh::g1_to_abi(hh::jac_mul(p, k, 4), out + i * HBH_G1_BYTES);
+    hh::g1_to_abi(hh::g1_mul_glv(p, k), out + i * HBH_G1_BYTES);
   });
   return bad ? host_fail(HBH_ERR_ARG, "coordinate >= p") : HBH_OK;
 }
@@ -489,7 +809,7 @@ int hbh_host_g2_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_
     }
     uint64_t k[4];
     scalar_limbs(scalars + i * 32, k);
-    hh::g2_to_abi(hh::jac_mul(p, k, 4), out + i * HBH_G2_BYTES);
+    hh::g2_to_abi(hh::g2_mul_gls(p, k), out + i * HBH_G2_BYTES);
   });
   return bad ? host_fail(HBH_ERR_ARG, "coordinate >= p") : HBH_OK;
 }
@@ -513,11 +833,7 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
     return host_fail(HBH_ERR_ARG, "null pointer");
   for (size_t i = 0; i < n; i++)
     if (offsets[i + 1] < offsets[i]) return host_fail(HBH_ERR_ARG, "offsets not ascending");
-  static const uint64_t G1_CANON[12] = {0xfb3af00adb22c6bbull, 0x6c55e83ff97a1aefull, 0xa14e3a3f171bac58ull,
-                                        0xc3688c4f9774b905ull, 0x2695638c4fa9ac0full, 0x17f1d3a73197d794ull,
-                                        0x0caa232946c5e7e1ull, 0xd03cc744a2888ae4ull, 0x00db18cb2c04b3edull,
-                                        0xfcf5e095d5d00af6ull, 0xa09e30ed741d8ae4ull, 0x08b3f481e3aaa0f1ull};
-  const hh::Jac<hh::Fq> g1 = {hh::fq_from_canon(G1_CANON), hh::fq_from_canon(G1_CANON + 6), hh::fq_one()};
+  hh::g1_comb();  // build the fixed-base table before the workers share it
   std::atomic<int> bad(0);
   hh::parallel_for(n, threads, [&](size_t i) {
     hh::Jac<hh::Fq> pk;
@@ -527,17 +843,22 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
     }
     uint64_t r[4];
     scalar_limbs(nonces + i * 32, r);
+    hh::reduce_r(r);
+    // U = g1 r (comb) and pk r (GLV), made affine with one inversion
+    const hh::Jac<hh::Fq> jp[2] = {hh::g1_mul_gen(r), hh::g1_mul_glv(pk, r)};
+    hh::Aff<hh::Fq> ap[2];
+    hh::jac_batch_affine(jp, ap, 2);
     uint8_t* u = u_out + i * HBH_G1_BYTES;
-    hh::g1_to_abi(hh::jac_mul(g1, r, 4), u);  // U = g1 r
+    hh::g1_aff_to_abi(ap[0], u);
     uint8_t g[HBH_G1_BYTES];
-    hh::g1_to_abi(hh::jac_mul(pk, r, 4), g);  // pk r
+    hh::g1_aff_to_abi(ap[1], g);
     const size_t len = offsets[i + 1] - offsets[i];
     hh::xor_with_hash(g, data + offsets[i], len, v_out + offsets[i]);  // V = msg xor stream
-    uint8_t h[HBH_G2_BYTES];
-    hh::hash_g1_g2(u, v_out + offsets[i], len, h);
-    hh::Jac<hh::Fq2> hp;
-    hh::g2_from_abi(h, hp);
-    hh::g2_to_abi(hh::jac_mul(hp, r, 4), w_out + i * HBH_G2_BYTES);  // W = hash_g1_g2(U, V) r
+    // W = hash_g1_g2(U, V) r = [KCOF] Q_bp r = [KCOF r mod r] Q_bp: one GLS multiplication
+    const std::vector<uint8_t> m = hh::g1_g2_msg(u, v_out + offsets[i], len);
+    uint64_t kr[4];
+    hh::fr_mul(hh::KCOF, r, kr);
+    hh::g2_to_abi(hh::g2_mul_gls(hh::hash_g2_bp(m.data(), m.size()), kr), w_out + i * HBH_G2_BYTES);
   });
   return bad ? host_fail(HBH_ERR_ARG, "coordinate >= p") : HBH_OK;
 }

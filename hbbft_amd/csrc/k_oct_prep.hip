@@ -1,9 +1,9 @@
 // Line tables of shared G2 points on lane octos (the TABLE side of every pairing kernel).
 //
-// k_pair_prep's serial 68-step walk of one point with the lane-octo doubling and addition steps
-// (ofp.hpp: 3 and 5 rounds of four Fp2 products instead of the lane quad's 6 and 7), eight lanes per
-// point; pair 0 of each octo writes the table in k_pair_prep's layout (c0, c1, c4 per lane component,
-// PL_Q4 16-byte chunks), which every verify kernel reads unchanged.
+// The serial 68-step walk of one shared point (63 doublings + 5 additions of |x|) with the lane-octo
+// doubling and addition steps (ofp.hpp: 3 and 5 rounds of four Fp2 products), eight lanes per point;
+// pair 0 of each octo writes the table (c0, c1, c4 per step and lane component, PL_Q4 16-byte chunks,
+// pair_side.hpp), which every verify kernel reads unchanged.
 #include "launch.hpp"
 #include "pair_side.hpp"
 #include "ofp.hpp"

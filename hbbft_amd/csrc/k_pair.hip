@@ -8,7 +8,7 @@
 //
 // Each G2 side is one of
 //   TABLE: Q is shared by many checks (H per document, W / H_uv per ciphertext): its 68 lines are
-//          computed once by k_pair_prep into a table that the checks of a wave read as broadcasts;
+//          computed once by k_oct_prep (k_oct_prep.hip) into a table that the checks of a wave read as broadcasts;
 //   WALK : Q is per check (sigma_i, or both sides of Ciphertext::verify): T walks inside the Miller
 //          loop in registers -- no per-share line table ever reaches HBM.
 // The whole check is one kernel: the Fp12 state never leaves the CU.  During the final
@@ -105,63 +105,11 @@ __global__ void __launch_bounds__(256, 2) k_pair_verify(PairArgs a) {
   if (lp_even() && a.verdict) a.verdict[i] = one ? 1 : 0;
 }
 
-// ---------------------------------------------------------------- line tables of shared G2 points
-// One lane QUAD per shared point (qfp.hpp: the walk's independent products split over two lane
-// pairs, 6 product rounds per doubling instead of 11 products): a batch's tables are a few dozen
-// waves, so the 68-step walk's latency is the kernel's time.  Pair 0 of the quad writes the table.
-__global__ void __launch_bounds__(256, 1) k_pair_prep(int n, const uint32_t* __restrict__ q, int4* __restrict__ lines,
-                                                      uint8_t* __restrict__ qinf) {
-  const int j = (int)((blockIdx.x * 256u + threadIdx.x) >> 2);
-  if (j >= n) return;
-  const uint32_t* w = q + (size_t)j * 48;
-  const bool inf = lp_both(words_zero(w + (lp_even() ? 0 : 12), 12) && words_zero(w + (lp_even() ? 24 : 36), 12));
-  Fp xQ, yQ;
-  h_g2_load(w, xQ, yQ);
-  if (inf) {
-    xQ = h_one();
-    yQ = h_one();
-  }
-  const bool writer = !q_hi();
-  if (writer && lp_even()) qinf[j] = inf ? 1 : 0;
-  HJac T{xQ, yQ, h_one()};
-  int4* base = lines + (size_t)j * PAIR_STEPS * 2 * PL_Q4 + (lp_even() ? 0 : PL_Q4);
-  int step = 0;
-#pragma unroll 1
-  for (int b = 62; b >= 0; b--) {
-#pragma unroll 1
-    for (int add = 0; add < (((hb::X_ABS >> b) & 1) ? 2 : 1); add++) {
-      const HLine l = add ? h_add_step_q(T, xQ, yQ) : h_dbl_step_q(T);
-      if (writer) {
-        int32_t o[4 * PL_Q4];
-#pragma unroll
-        for (int k = 0; k < NL; k++) {
-          o[k] = l.c0.l[k];
-          o[NL + k] = l.c1.l[k];
-          o[2 * NL + k] = l.c4.l[k];
-        }
-        o[3 * NL] = 0;
-        o[3 * NL + 1] = 0;
-        int4* dst = base + (size_t)step * 2 * PL_Q4;
-#pragma unroll
-        for (int k = 0; k < PL_Q4; k++) dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
-      }
-      step++;
-    }
-  }
-}
-
 }  // namespace hbs
 
 namespace hbl {
 
 size_t pair_table_bytes(size_t nq) { return nq * (size_t)hbs::PAIR_STEPS * 2 * hbs::PL_Q4 * 16; }
-
-hipError_t pair_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* qinf) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hbs::k_pair_prep, dim3((unsigned)((4 * (size_t)n + 255) / 256)), dim3(256), 0, s, n,
-                     (const uint32_t*)q, (int4*)lines, qinf);
-  return hipGetLastError();
-}
 
 hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairSideDesc& d2, int flags,
                        uint8_t* verdict, uint32_t* value_out) {

@@ -23,13 +23,13 @@
 namespace hbs {
 
 constexpr int WV_STRIDE = 36;  // words per slot (2 components x 16, +4 against bank conflicts)
-constexpr int WV_LINE_Q4 = 11;  // k_pair_prep table: 16-byte chunks per (line, lane component)
+constexpr int WV_LINE_Q4 = 11;  // k_oct_prep table: 16-byte chunks per (line, lane component)
 constexpr uint32_t WV_ZW[NL] = {0};
 
 struct WaveSide {
   const uint32_t* p;    // G1 points (24 words), nullptr = the generator
   const uint32_t* q;    // WALK: G2 points (48 words)
-  const int4* lines;    // TABLE: k_pair_prep line tables (nullptr = WALK)
+  const int4* lines;    // TABLE: k_oct_prep line tables (nullptr = WALK)
   const uint8_t* qinf;  // TABLE: 1 = table point at infinity
   const uint32_t* idx;  // Q index per check (nullptr = identity)
   uint32_t nq;

@@ -12,7 +12,7 @@ namespace hbl {
 constexpr int HBL_DUPLICATE = 5;  // == HBH_ERR_DUPLICATE_ENTRY
 constexpr int HBL_BAD_INDEX = 1;  // == HBH_ERR_ARG
 // --------------------------------------------------------------- lane-pair pairing (k_pair.hip)
-// One side of a pairing-equality check.  TABLE side: `lines`/`qinf` from pair_prep over the nq
+// One side of a pairing-equality check.  TABLE side: `lines`/`qinf` from oct_prep over the nq
 // shared G2 points, `idx` picks the table per check.  WALK side (lines == nullptr): `q` holds G2
 // points walked inside the Miller loop, `idx` picks the point per check (nullptr = identity).
 // p == nullptr means the G1 generator for every check.  Indices >= nq yield verdict 0.
@@ -25,7 +25,6 @@ struct PairSideDesc {
   size_t nq;
 };
 size_t pair_table_bytes(size_t nq);
-hipError_t pair_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* qinf);
 // the same tables from lane octos (k_oct_prep.hip: eight lanes per point)
 hipError_t oct_prep(hipStream_t s, int n, const void* q, void* lines, uint8_t* qinf);
 // flags: bit 0 negates P2 (pairing equality), bit 1 conjugates f (single pairing value, with
@@ -36,7 +35,7 @@ hipError_t pair_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairS
 // --------------------------------------------------------------- lane-quad pairing (k_quad.hip)
 // The same verdicts / values as pair_verify with FOUR lanes per check (two lane pairs splitting
 // each step's independent products): the mid-size batches, one wave per SIMD at 16,384 checks.
-// TABLE sides read pair_prep tables.
+// TABLE sides read oct_prep tables.
 hipError_t quad_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
                        uint8_t* verdict, uint32_t* value_out);
 
@@ -48,7 +47,7 @@ hipError_t oct_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSi
 
 // --------------------------------------------------------------- wave-per-check pairing (k_wave.hip)
 // The same verdicts / values as pair_verify with one 64-lane workgroup per check (the latency
-// kernel: a check's Fp2 products run on 32 lane pairs side by side).  TABLE sides read pair_prep
+// kernel: a check's Fp2 products run on 32 lane pairs side by side).  TABLE sides read oct_prep
 // tables; wave_lds_bytes() of LDS per workgroup.
 size_t wave_lds_bytes();
 hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,

@@ -63,7 +63,7 @@ HP_D H12 unstash12(const uint32_t* __restrict__ s) {
 struct PairSide {
   const uint32_t* p;    // G1 points, 24 words each; nullptr: the generator g1 for every check
   const uint32_t* q;    // WALK: G2 points, 48 words each
-  const int4* lines;    // TABLE: line tables written by k_pair_prep
+  const int4* lines;    // TABLE: line tables written by k_oct_prep
   const uint8_t* qinf;  // TABLE: 1 = table point at infinity
   const uint32_t* idx;  // Q index per check (nullptr = identity)
   uint32_t nq;          // number of Q points / tables

@@ -1,4 +1,5 @@
-// Signed-limb BLS12-381 Fp / Fp2 for the lane-cooperative pairing (k_lc.hip), namespace hbs.
+// Signed-limb BLS12-381 Fp / Fp2 (namespace hbs): the base of the lane-pair tower (pfp.hpp) and of the
+// lane-quad G1 kernels (k_g1quad.hip).
 //
 // Representation: 14 int32 limbs of radix 2^28, value = sum l[i] 2^(28 i) (signed), Montgomery
 // form with R = 2^392.  "Normalised": l[0..12] in [0, 2^28), l[13] signed.
@@ -24,9 +25,9 @@
 #define HS_HD inline
 #endif
 
-// fp_mul / fp_sqr linkage: inlined by default (lane-cooperative kernels); a translation unit may
-// define HS_MULFN as a static non-inlined device function to keep one copy hot in the
-// instruction cache (the one-thread-per-check kernel of k_thread.hip).
+// Product linkage: inlined by default; a translation unit may define HS_MULFN as a static
+// non-inlined device function to keep one copy of the product hot in the instruction cache (the
+// pairing kernels k_pair.hip, k_quad_g*.hip, k_oct_g*.hip and k_interp_pair.hip do).
 #ifndef HS_MULFN
 #define HS_MULFN HS_HD
 #endif
