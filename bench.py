@@ -445,6 +445,8 @@ def main():
     ap.add_argument("--batch", type=int, default=NDOCS * N_NODES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
+    ap.add_argument("--no-node-round", action="store_true",
+                    help="dkg workload: skip the one-node SyncKeyGen round (node_round)")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
     ap.add_argument("--impl", choices=["pair", "wave", "quad", "oct", "auto"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
@@ -863,6 +865,7 @@ def run_dkg(args, eng, world, rank, dev):
             ts_.append((time.perf_counter() - t0) * 1e3)
         commit_ms[k] = statistics.median(ts_)
     enc = dkg_encrypt_cost(eng, n_nodes, t)
+    node_round = dkg_node_round(eng, n_nodes, t) if rank == 0 and not args.no_node_round else None
     ms = _max_over_ranks(dev_ms, world, dev)
     host_ms = _max_over_ranks(statistics.median(times), world, dev)
     per_rank = gather_per_rank({"rank": rank, "device_ms": dev_ms, "host_ms": statistics.median(times), "ok": ok,
@@ -898,6 +901,7 @@ def run_dkg(args, eng, world, rank, dev):
                                  "upload of indices and values"},
             "host_to_host_ms": host_ms, "row_build_ms": row_ms, "rows": len(nodes) * n_nodes,
             "encrypt": enc,
+            "node_round": node_round,
             "bivar_commitment_ms": {"1 part (595 points)": commit_ms[1], "100 parts (59,500 points)": commit_ms[n_nodes],
                                     "note": "BivarPoly::commitment on the comb table (hbh_g1_mul_gen), host-to-host"},
             "data_gen_s": round(gen_s, 2), "verdicts_ok": ok, "per_rank": per_rank,
@@ -942,6 +946,63 @@ def dkg_encrypt_cost(eng, n_nodes, t, reps=3):
     out["host_threads"] = threads
     out["note"] = ("host stage, %d threads; one Part = %d row encryptions, one Ack = %d value encryptions; "
                    "per_node_dkg_ms = one Part + %d Acks" % (threads, n_nodes, n_nodes, n_nodes))
+    return out
+
+
+def dkg_node_round(eng, n_nodes, t, seed=5):
+    """One node's whole SyncKeyGen round through hbbft_amd.sync_key_gen (src/sync_key_gen.rs): generate
+    our Part (SyncKeyGen::new: BivarPoly::random, its commitment, N row encryptions, :323-357), handle
+    the N Parts (decrypt our row of each, Poly::commitment == row(x), one Ack of N value encryptions per
+    valid Part, :372-392, 481-512) and the N^2 Acks (decrypt our value of each, evaluate == g1 val,
+    :398-404, 515-547) -- every SecretKey::decrypt, encrypt_with_rng, hash and check a node runs.
+    Setup (untimed): the other nodes' Parts and Acks; in each only the ciphertext addressed to our node
+    is real (the others are a copy of it: our node reads only its own, checks only the count).
+    Returns the timings and whether every outcome is fault-free."""
+    from hbbft_amd import hoststage
+    from hbbft_amd.sync_key_gen import SyncKeyGen, Part, Ack, Ciphertext, coeff_pos, ser_row, ser_val
+    rng = random.Random(seed)
+    g1 = g1a_abi()
+    sks = [rng.randrange(1, R_ORDER) for _ in range(n_nodes)]
+    pks = dict(enumerate(eng.g1_mul([g1] * n_nodes, sks)))
+    our = 0
+    ox = our + 1
+    npos = (t + 1) * (t + 2) // 2
+    coefs = [[rng.randrange(R_ORDER) for _ in range(npos)] for _ in range(n_nodes)]
+    flat = eng.g1_mul_gen([c for cs in coefs for c in cs])
+    commits = [flat[p * npos:(p + 1) * npos] for p in range(n_nodes)]
+    ys = list(range(1, n_nodes + 1))
+    # our row of part p: row_p(ox)_a = sum_b c_p(a, b) ox^b; the values acks carry for us: f_p(y, ox)
+    our_rows = [[poly_eval([coefs[p][coeff_pos(a, b)] for b in range(t + 1)], ox) for a in range(t + 1)]
+                for p in range(n_nodes)]
+    our_vals = hoststage.fr_poly_eval(our_rows, ys)
+    threads = hoststage.host_threads()
+    row_cts = hoststage.encrypt([pks[our]], [ser_row(r) for r in our_rows],
+                                [rng.randrange(1, R_ORDER) for _ in range(n_nodes)], threads)
+    val_cts = hoststage.encrypt([pks[our]], [ser_val(v) for vs in our_vals for v in vs],
+                                [rng.randrange(1, R_ORDER) for _ in range(n_nodes * n_nodes)], threads)
+    parts = [(p, Part(t, commits[p], [Ciphertext(*row_cts[p])] * n_nodes)) for p in range(n_nodes)]
+    acks = [(y - 1, Ack(p, [Ciphertext(*val_cts[p * n_nodes + y - 1])] * n_nodes))
+            for p in range(n_nodes) for y in ys]
+    out = {}
+    t0 = time.perf_counter()
+    _, own_part = SyncKeyGen.new(our, sks[our], pks, t, eng, rng=random.Random(seed + 1), threads=threads)
+    out["generate_part_ms"] = (time.perf_counter() - t0) * 1e3
+    kg = SyncKeyGen(our, sks[our], pks, t, eng, threads=threads)
+    t0 = time.perf_counter()
+    p_out = kg.handle_parts(parts, rng=random.Random(seed + 2))
+    out["handle_parts_ms"] = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    a_out = kg.handle_acks(acks)
+    out["handle_acks_ms"] = (time.perf_counter() - t0) * 1e3
+    out["node_round_ms"] = out["generate_part_ms"] + out["handle_parts_ms"] + out["handle_acks_ms"]
+    ok = (own_part is not None and len(own_part.rows) == n_nodes
+          and all(o.valid and o.ack is not None and len(o.ack.values) == n_nodes for o in p_out)
+          and all(o.valid for o in a_out) and kg.is_ready())
+    out.update({"outcomes_ok": ok, "host_threads": threads, "encryptions": n_nodes + n_nodes * n_nodes,
+                "decryptions": n_nodes + n_nodes * n_nodes, "parts": n_nodes, "acks": n_nodes * n_nodes,
+                "note": "one node's SyncKeyGen round through hbbft_amd.sync_key_gen, host-to-host: host stage "
+                        "(hash_g1_g2, encrypt_with_rng, U*sk, Fr Horner) on %d threads, engine calls "
+                        "(Ciphertext::verify, Poly::commitment, ack checks) on the GPU" % threads})
     return out
 
 

@@ -376,6 +376,21 @@ static void fr_mul(const uint64_t* a, const uint64_t* b, uint64_t* out) {
   fr_mont(a, b, t);
   fr_mont(t, R2R, out);
 }
+static void fr_to_mont(const uint64_t* a, uint64_t* out) {
+  static const uint64_t R2R[4] = {0xc999e990f3f29c6dull, 0x2b6cedcb87925c23ull, 0x05d314967254398full,
+                                  0x0748d9d99f59ff11ull};
+  fr_mont(a, R2R, out);
+}
+// a + b mod r (a, b < r)
+static void fr_add(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+  uint64_t c = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 s = (u128)a[i] + b[i] + c;
+    out[i] = (uint64_t)s;
+    c = (uint64_t)(s >> 64);
+  }
+  if (c || geq_r(out)) sub_r(out);
+}
 // k = q d + rem for a 64-bit d: k becomes q, returns rem
 static uint64_t divmod_u64(uint64_t* k, int nl, uint64_t d) {
   u128 rem = 0;
@@ -861,6 +876,38 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
     hh::g2_to_abi(hh::g2_mul_gls(hh::hash_g2_bp(m.data(), m.size()), kr), w_out + i * HBH_G2_BYTES);
   });
   return bad ? host_fail(HBH_ERR_ARG, "coordinate >= p") : HBH_OK;
+}
+
+int hbh_fr_poly_eval(size_t npoly, size_t ncoef, const uint8_t* coeffs, size_t npts, const uint64_t* xs, uint8_t* out,
+                     int threads) {
+  if (npoly == 0 || npts == 0) return HBH_OK;
+  if (!xs || !out || (ncoef && !coeffs)) return host_fail(HBH_ERR_ARG, "null pointer");
+  std::atomic<int> bad(0);
+  // Horner in the Montgomery domain (R = 2^256): x_k and the coefficients enter as a R, the result
+  // leaves through one product by 1
+  hh::parallel_for(npoly, threads, [&](size_t q) {
+    std::vector<uint64_t> c(4 * ncoef);
+    for (size_t j = 0; j < ncoef; j++) {
+      uint64_t v[4];
+      scalar_limbs(coeffs + (q * ncoef + j) * 32, v);
+      if (hh::geq_r(v)) bad = 1;
+      hh::fr_to_mont(v, &c[4 * j]);
+    }
+    for (size_t k = 0; k < npts; k++) {
+      uint64_t x[4] = {xs[k], 0, 0, 0}, xm[4], acc[4] = {0, 0, 0, 0};
+      hh::reduce_r(x);
+      hh::fr_to_mont(x, xm);
+      for (size_t j = ncoef; j-- > 0;) {
+        uint64_t t[4];
+        hh::fr_mont(acc, xm, t);
+        hh::fr_add(t, &c[4 * j], acc);
+      }
+      uint64_t one[4] = {1, 0, 0, 0}, res[4];
+      hh::fr_mont(acc, one, res);
+      memcpy(out + (q * npts + k) * 32, res, 32);
+    }
+  });
+  return bad ? host_fail(HBH_ERR_ARG, "coefficient >= r") : HBH_OK;
 }
 
 }  // extern "C"

@@ -164,3 +164,23 @@ def encrypt(pks, msgs, nonces, threads=0):
     raw_v = bytes(ov)[:len(data)]
     us, ws = _split(bytes(ou), G1_BYTES, n), _split(bytes(ow), G2_BYTES, n)
     return [(us[i], raw_v[int(offs[i]):int(offs[i + 1])], ws[i]) for i in range(n)]
+
+
+def fr_poly_eval(polys, xs, threads=0):
+    """Poly::evaluate over Fr (hbh_fr_poly_eval): [[poly(x) for x in xs] for poly in polys]; every
+    polynomial is a coefficient list (constant term first) of one common length, coefficients < r."""
+    npoly = len(polys)
+    if npoly == 0 or not xs:
+        return [[] for _ in polys]
+    ncoef = len(polys[0])
+    if any(len(c) != ncoef for c in polys):
+        raise ValueError("polynomials of different lengths")
+    kc, pc = _buf(b"".join(int(c).to_bytes(32, "little") for poly in polys for c in poly))
+    xa = np.asarray([int(x) for x in xs], dtype=np.uint64)
+    o, po = _out(npoly * len(xa) * 32)
+    check_host(_lib.lib().hbh_fr_poly_eval(npoly, ncoef, pc, len(xa), xa.ctypes.data_as(ctypes.c_void_p), po,
+                                           int(threads)))
+    raw = bytes(o)
+    m = len(xa)
+    return [[int.from_bytes(raw[32 * (q * m + k):32 * (q * m + k + 1)], "little") for k in range(m)]
+            for q in range(npoly)]

@@ -264,11 +264,12 @@ class SyncKeyGen:
         ncoef = (t + 1) * (t + 2) // 2
         coeffs = [rng.randrange(0, R_ORDER) for _ in range(ncoef)]
         commit = engine.g1_mul_gen(coeffs)
-        rows = []
-        for i in range(len(kg.pub_keys)):
-            x = i + 1
-            rows.append([sum(coeffs[coeff_pos(a, b)] * pow(x, b, R_ORDER) for b in range(t + 1)) % R_ORDER
-                         for a in range(t + 1)])
+        # row(x)_a = sum_b c(a, b) x^b for every node x (BivarPoly::row, sync_key_gen.rs:349-352):
+        # t+1 polynomials in x evaluated at the N node indices on the host stage
+        xs = [i + 1 for i in range(len(kg.pub_keys))]
+        ev = hoststage.fr_poly_eval([[coeffs[coeff_pos(a, b)] for b in range(t + 1)] for a in range(t + 1)], xs,
+                                    threads)
+        rows = [[ev[a][i] for a in range(t + 1)] for i in range(len(xs))]
         cts = _encrypt_batch(list(kg.pub_keys.values()), [ser_row(r) for r in rows], rng, threads)
         return kg, Part(t, commit, cts)
 
@@ -373,7 +374,8 @@ class SyncKeyGen:
                     ack_jobs.append((len(outs) - 1, sidx, r[1]))
         if ack_jobs:
             pks = list(self.pub_keys.values())
-            payloads = [ser_val(poly_eval(row, i + 1)) for _, _, row in ack_jobs for i in range(n)]
+            vals = _eval_rows([row for _, _, row in ack_jobs], [i + 1 for i in range(n)], self.threads)
+            payloads = [ser_val(v) for vs in vals for v in vs]
             cts = _encrypt_batch([pk for _ in ack_jobs for pk in pks], payloads, rng, self.threads)
             for j, (o, sidx, _) in enumerate(ack_jobs):
                 outs[o].ack = Ack(sidx, cts[j * n:(j + 1) * n])
@@ -487,6 +489,16 @@ class SyncKeyGen:
                 samples = sorted(part.values.items())[: t + 1]
                 sk = (sk + interpolate_at_zero(samples)) % R_ORDER
         return PublicKeySet(commit), sk
+
+
+def _eval_rows(rows, xs, threads=0):
+    """[[Poly::evaluate(row, x) for x in xs] for row in rows] on the host stage (hbh_fr_poly_eval),
+    one call per row length (Parts of different degrees give rows of different lengths)."""
+    out = [None] * len(rows)
+    for ln, js in _by_degree(range(len(rows)), lambda j: len(rows[j])).items():
+        for j, v in zip(js, hoststage.fr_poly_eval([rows[j] for j in js], xs, threads)):
+            out[j] = v
+    return out
 
 
 def _by_degree(items, degree):

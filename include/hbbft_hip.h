@@ -275,6 +275,10 @@ int hbh_g2_decompress(hbh_engine* eng, size_t n, const uint8_t* in, uint8_t* out
  *                     U = g1 r, V = msg xor stream(pk r), W = hash_g1_g2(U, V) r
  *                     (sync_key_gen.rs:346-357,386-390; honey_badger/epoch_state.rs:224-237);
  *                     pks holds one key, or one per item when pk_per_item != 0
+ *   hbh_fr_poly_eval  Poly::evaluate over Fr for many polynomials and points: out[p * npts + k] =
+ *                     sum_j coeffs[p * ncoef + j] x_k^j mod r (32 B LE scalars in and out, coefficients
+ *                     < r; xs are small node indices).  SyncKeyGen's rows of BivarPoly::row(x)
+ *                     (sync_key_gen.rs:349-352) and the Ack values row.evaluate(i + 1) (:386-390)
  *   hbh_host_threads  the worker count `threads` = 0 means: the CPUs this process may use
  *                     (affinity mask, cgroup v2 cpu.max quota, HBH_HOST_THREADS / OMP_NUM_THREADS) */
 const char* hbh_host_last_error(void);
@@ -292,6 +296,8 @@ int hbh_host_g2_mul(size_t n, const uint8_t* pts, const uint8_t* scalars, uint8_
 int hbh_host_g1_add(size_t n, const uint8_t* a, const uint8_t* b, uint8_t* out);
 int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* data, const size_t* offsets,
                 const uint8_t* nonces, uint8_t* u_out, uint8_t* v_out, uint8_t* w_out, int threads);
+int hbh_fr_poly_eval(size_t npoly, size_t ncoef, const uint8_t* coeffs, size_t npts, const uint64_t* xs, uint8_t* out,
+                     int threads);
 
 /* ---------------------------------------------------------------- implementation selection
  * Pairing implementations with identical verdicts (tests/test_gpu_pairing.py cross-checks them

@@ -96,7 +96,7 @@ def test_dkg_two_ranks_match_one_rank():
     """configs[3] network scope split by checking node over two ranks (src/sync_key_gen.rs:515-547):
     the per-rank acks sum to the total, every node is checked exactly once, and the gathered
     verdicts (per node, in node order) equal the one-rank run's."""
-    d1, d2 = _strong_pair("dkg", ["--dkg-nodes", "6"])
+    d1, d2 = _strong_pair("dkg", ["--dkg-nodes", "6", "--no-node-round"])
     assert d1["n_gpus"] == 1 and d2["n_gpus"] == 2
     assert d1["verdicts_ok"] is True and d2["verdicts_ok"] is True
     assert d2["config"]["total_acks"] == d1["config"]["total_acks"] == 6 * 100 * 100

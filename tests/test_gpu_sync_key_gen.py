@@ -216,3 +216,45 @@ def test_mixed_degree_parts(engine):
     assert all(nodes[0].parts[p].is_complete(t) for p in range(n))
     pks, sk = nodes[0].generate()
     assert len(pks.commit) == t + 2  # degree-2 part's row(0) extends the key's commitment
+
+
+def _pt1(b):
+    return None if b == bytes(96) else (int.from_bytes(b[:48], "little"), int.from_bytes(b[48:], "little"))
+
+
+def _pt2(b):
+    if b == bytes(192):
+        return None
+    w = [int.from_bytes(b[48 * k:48 * (k + 1)], "little") for k in range(4)]
+    return ((w[0], w[1]), (w[2], w[3]))
+
+
+def test_encrypt_decrypt_batches_match_oracle(engine):
+    """encrypt_with_rng on fixed nonces (hbh_encrypt: comb U = g1 r, GLV pk r, W = [KCOF r] Q_bp) and
+    SecretKey::decrypt over a batch (_decrypt_batch: host hash_g1_g2, engine Ciphertext::verify,
+    host GLV U sk + XOR) against oracle/tc.py (src/sync_key_gen.rs:346-357, 386-390, 503-506, 535-538):
+    byte-identical (U, V, W) for 32-byte Ack values and 1,096-byte Part rows (the two |V| branches of
+    hash_g1_g2) plus 0 / 64 / 65-byte edge messages; plaintexts recovered; tampered U, V or W -> None,
+    as the oracle's Ciphertext::verify rejects them."""
+    from oracle import tc
+    from hbbft_amd.sync_key_gen import _decrypt_batch, ser_row, ser_val
+    rng = random.Random(77)
+    sk = rng.randrange(1, R_ORDER)
+    pk = hoststage.g1_mul([G1_GEN], [sk])[0]
+    msgs = ([ser_val(rng.randrange(R_ORDER)) for _ in range(5)]
+            + [ser_row([rng.randrange(R_ORDER) for _ in range(34)]) for _ in range(3)] + [b"", bytes(64), bytes(65)])
+    nonces = [rng.randrange(1, R_ORDER) for _ in msgs]
+    got = hoststage.encrypt([pk], msgs, nonces, threads=4)
+    for (u, v, w), m, r in zip(got, msgs, nonces):
+        eu, ev, ew = tc.encrypt(_pt1(pk), m, r)
+        assert (_pt1(u), v, _pt2(w)) == (eu, ev, ew)
+    cts = [Ciphertext(u, v, w) for u, v, w in got]
+    # tampered copies: V byte flipped, W of another ciphertext, U of another ciphertext
+    bad = [Ciphertext(cts[0].u, bytes([cts[0].v[0] ^ 1]) + cts[0].v[1:], cts[0].w),
+           Ciphertext(cts[6].u, cts[6].v, cts[1].w),
+           Ciphertext(cts[2].u, cts[7].v, cts[7].w)]
+    for c in bad:
+        assert not tc.ciphertext_verify((_pt1(c.u), c.v, _pt2(c.w)))
+    plain = _decrypt_batch(engine, sk, cts + bad, threads=4)
+    assert plain[:len(msgs)] == msgs
+    assert plain[len(msgs):] == [None] * len(bad)

@@ -53,6 +53,52 @@ def test_hash_g2_matches_oracle_and_golden(hs):
     assert hs.hash_g2(msgs) == [abi_g2(tc.hash_g2(m)) for m in msgs]
 
 
+def test_hash_g2_many_messages(hs):
+    """Round 5's hash path (norm-method square root, Budroni-Pintore image + GLS multiplication by
+    h2 s^-1 mod r) against the oracle's textbook G2::rand (Fq2 exponentiation square root, double-and-add
+    by the 636-bit h2) on 160 seeded messages of lengths 0..300: each hash samples ~2 curve x's, so
+    the non-square / retry branch and both `greatest` choices are exercised many times over."""
+    rng = random.Random(2024)
+    msgs = [bytes(rng.randrange(256) for _ in range(rng.randrange(0, 301))) for _ in range(160)]
+    assert hs.hash_g2(msgs, threads=2) == [abi_g2(tc.hash_g2(m)) for m in msgs]
+
+
+def test_scalar_mul_edge_scalars(hs):
+    """GLV (G1: k = k2 lambda + k1, lambda = z^2 - 1) and GLS (G2: base-|z| digits) split boundaries:
+    scalars around lambda, |z|^i, r and 2^256 against the oracle's double-and-add of k mod r."""
+    z, lam = C.X_ABS, C.X_ABS ** 2 - 1
+    ks = [0, 1, 2, 15, 16, 17, lam - 1, lam, lam + 1, lam * lam - 1, lam * lam, lam * (lam + 1),
+          z - 1, z, z + 1, z ** 2, z ** 3 - 1, z ** 3, z ** 3 + 1, C.R - 1, C.R, C.R + 1, 2 * C.R - 1, 2 * C.R,
+          (1 << 255) - 1, 1 << 255, (1 << 256) - 1, int("5" * 76) % (1 << 256)]
+    rng = random.Random(8)
+    ks += [rng.randrange(0, 1 << 256) for _ in range(12)]
+    p1 = C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))
+    p2 = C.g2_mul(C.G2_GEN, rng.randrange(1, C.R))
+    assert hs.g1_mul([abi_g1(p1)] * len(ks), ks, threads=2) == [abi_g1(C.g1_mul(p1, k % C.R)) for k in ks]
+    assert hs.g2_mul([abi_g2(p2)] * len(ks), ks, threads=2) == [abi_g2(C.g2_mul(p2, k % C.R)) for k in ks]
+    # the point at infinity stays all-zero
+    assert hs.g1_mul([bytes(96)], [5]) == [bytes(96)] and hs.g2_mul([bytes(192)], [5]) == [bytes(192)]
+
+
+def test_fr_poly_eval(hs):
+    """Poly::evaluate over Fr (hbh_fr_poly_eval, SyncKeyGen's rows and Ack values) against Horner in
+    Python: random degree-33 polynomials, the all-(r-1) polynomial, x = 0, 1, 100 and 2^64 - 1."""
+    rng = random.Random(9)
+    polys = [[rng.randrange(C.R) for _ in range(34)] for _ in range(9)] + [[C.R - 1] * 34, [0] * 34]
+    xs = [0, 1, 2, 100, (1 << 64) - 1]
+
+    def ev(c, x):
+        r = 0
+        for a in reversed(c):
+            r = (r * x + a) % C.R
+        return r
+    assert hs.fr_poly_eval(polys, xs, threads=2) == [[ev(c, x) for x in xs] for c in polys]
+    assert hs.fr_poly_eval([[7]], [3]) == [[7]]
+    from hbbft_amd._lib import HbhError
+    with pytest.raises(HbhError):
+        hs.fr_poly_eval([[C.R]], [1])
+
+
 def test_hash_g1_g2_both_branches(hs):
     rng = random.Random(11)
     us = [C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)) for _ in range(3)]
