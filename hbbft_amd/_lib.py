@@ -82,6 +82,8 @@ SIGNATURES = [
     ("hbh_host_g1_add", _I, [_SZ, _P, _P, _P]),
     ("hbh_encrypt", _I, [_SZ, _P, _I, _P, _P, _P, _P, _P, _P, _I]),
     ("hbh_fr_poly_eval", _I, [_SZ, _SZ, _P, _SZ, _P, _P, _I]),
+    ("hbh_hash_g1_g2_bp", _I, [_SZ, _P, _P, _P, _P, _I]),
+    ("hbh_hash_bp_g1", _I, [_P]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
 IMPL_AUTO, IMPL_PAIR, IMPL_WAVE, IMPL_QUAD, IMPL_OCT = 3, 4, 5, 6, 7   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)

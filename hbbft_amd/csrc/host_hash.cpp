@@ -25,6 +25,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/hbbft_hip.h"
@@ -601,6 +602,36 @@ static Jac<Fq> g1_mul_gen(const uint64_t* k_in) {
   return r;
 }
 
+// 4-bit fixed-base comb of a G1 point used by many multiplications in one call (encrypt_with_rng's pk r
+// when a batch encrypts to a few keys, as a SyncKeyGen node does: 100 values to each of N keys):
+// T[w * 15 + d - 1] = d 16^w P, 64 x 15 affine points from one batch normalisation; [k] P = 64 mixed
+// additions instead of GLV's 129 doublings + ~43 additions
+static std::vector<Aff<Fq>> comb4_build(const Jac<Fq>& p) {
+  std::vector<Jac<Fq>> j(64 * 16);
+  Jac<Fq> base = p;
+  for (int w = 0; w < 64; w++) {
+    j[w * 16] = base;
+    for (int d = 1; d < 16; d++) j[w * 16 + d] = jac_add(j[w * 16 + d - 1], base);  // (d + 1) base
+    base = j[w * 16 + 15];                                                           // 16 base
+  }
+  std::vector<Aff<Fq>> a(64 * 16), t(64 * 15);
+  jac_batch_affine(j.data(), a.data(), j.size());
+  for (int w = 0; w < 64; w++)
+    for (int d = 0; d < 15; d++) t[w * 15 + d] = a[w * 16 + d];
+  return t;
+}
+static Jac<Fq> comb4_mul(const std::vector<Aff<Fq>>& t, const uint64_t* k_in) {
+  uint64_t k[4];
+  memcpy(k, k_in, 32);
+  reduce_r(k);
+  Jac<Fq> r = jac_inf<Fq>();
+  for (int w = 0; w < 64; w++) {
+    const int d = (int)((k[w >> 4] >> (4 * (w & 15))) & 15);
+    if (d && !t[w * 15 + d - 1].inf) r = jac_add_aff(r, t[w * 15 + d - 1].x, t[w * 15 + d - 1].y);
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------- hash to G2
 // pairing 0.14 G2::rand up to the cofactor multiplication: the first sampled curve point (x, y) whose
 // h2 multiple is not O, returned as Q_bp (h2 (x, y) = [KCOF] Q_bp; Q_bp = O exactly when h2 (x, y) = O)
@@ -750,6 +781,38 @@ int hbh_hash_g1_g2(size_t n, const uint8_t* u, const uint8_t* data, const size_t
   return HBH_OK;
 }
 
+int hbh_hash_g1_g2_bp(size_t n, const uint8_t* u, const uint8_t* data, const size_t* offsets, uint8_t* out,
+                      int threads) {
+  if (n == 0) return HBH_OK;
+  if (!u || !offsets || !out || (!data && offsets[n] != 0)) return host_fail(HBH_ERR_ARG, "null pointer");
+  for (size_t i = 0; i < n; i++)
+    if (offsets[i + 1] < offsets[i]) return host_fail(HBH_ERR_ARG, "offsets not ascending");
+  hh::parallel_for(n, threads, [&](size_t i) {
+    const std::vector<uint8_t> m = hh::g1_g2_msg(u + i * HBH_G1_BYTES, data + offsets[i], offsets[i + 1] - offsets[i]);
+    hh::g2_to_abi(hh::hash_g2_bp(m.data(), m.size()), out + i * HBH_G2_BYTES);
+  });
+  return HBH_OK;
+}
+
+int hbh_hash_bp_g1(uint8_t* out) {
+  if (!out) return host_fail(HBH_ERR_ARG, "null pointer");
+  // [KCOF^-1 mod r] g1 = [KCOF^(r-2)] g1: exponentiation in Fr by square-and-multiply on fr_mul
+  static const uint64_t RM2[4] = {0xfffffffeffffffffull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                                  0x73eda753299d7d48ull};
+  uint64_t acc[4] = {1, 0, 0, 0};
+  for (int b = 254; b >= 0; b--) {
+    uint64_t t[4];
+    hh::fr_mul(acc, acc, t);
+    memcpy(acc, t, 32);
+    if ((RM2[b >> 6] >> (b & 63)) & 1) {
+      hh::fr_mul(acc, hh::KCOF, t);
+      memcpy(acc, t, 32);
+    }
+  }
+  hh::g1_to_abi(hh::g1_mul_gen(acc), out);
+  return HBH_OK;
+}
+
 int hbh_xor_with_hash(size_t n, const uint8_t* g, const uint8_t* data, const size_t* offsets, uint8_t* out,
                       int threads) {
   if (n == 0) return HBH_OK;
@@ -849,18 +912,42 @@ int hbh_encrypt(size_t n, const uint8_t* pks, int pk_per_item, const uint8_t* da
   for (size_t i = 0; i < n; i++)
     if (offsets[i + 1] < offsets[i]) return host_fail(HBH_ERR_ARG, "offsets not ascending");
   hh::g1_comb();  // build the fixed-base table before the workers share it
+  // keys: one, or one per item; a key that encrypts at least COMB_MIN items of this call gets a comb
+  const size_t COMB_MIN = 16;
+  std::vector<uint32_t> key_of(n, 0);
+  std::vector<const uint8_t*> keys;
+  if (pk_per_item) {
+    std::unordered_map<std::string, uint32_t> seen;
+    for (size_t i = 0; i < n; i++) {
+      const uint8_t* k = pks + i * HBH_G1_BYTES;
+      auto it = seen.emplace(std::string((const char*)k, HBH_G1_BYTES), (uint32_t)keys.size());
+      if (it.second) keys.push_back(k);
+      key_of[i] = it.first->second;
+    }
+  } else {
+    keys.push_back(pks);
+  }
+  std::vector<size_t> uses(keys.size(), 0);
+  for (size_t i = 0; i < n; i++) uses[key_of[i]]++;
+  std::vector<hh::Jac<hh::Fq>> key_pt(keys.size());
+  std::vector<std::vector<hh::Aff<hh::Fq>>> combs(keys.size());
   std::atomic<int> bad(0);
-  hh::parallel_for(n, threads, [&](size_t i) {
-    hh::Jac<hh::Fq> pk;
-    if (!hh::g1_from_abi(pks + (pk_per_item ? i : 0) * HBH_G1_BYTES, pk)) {
+  hh::parallel_for(keys.size(), threads, [&](size_t j) {
+    if (!hh::g1_from_abi(keys[j], key_pt[j])) {
       bad = 1;
       return;
     }
+    if (uses[j] >= COMB_MIN) combs[j] = hh::comb4_build(key_pt[j]);
+  });
+  if (bad) return host_fail(HBH_ERR_ARG, "coordinate >= p");
+  hh::parallel_for(n, threads, [&](size_t i) {
+    const uint32_t kj = key_of[i];
     uint64_t r[4];
     scalar_limbs(nonces + i * 32, r);
     hh::reduce_r(r);
-    // U = g1 r (comb) and pk r (GLV), made affine with one inversion
-    const hh::Jac<hh::Fq> jp[2] = {hh::g1_mul_gen(r), hh::g1_mul_glv(pk, r)};
+    // U = g1 r (g1's comb) and pk r (the key's comb, or GLV), made affine with one inversion
+    const hh::Jac<hh::Fq> jp[2] = {hh::g1_mul_gen(r),
+                                   combs[kj].empty() ? hh::g1_mul_glv(key_pt[kj], r) : hh::comb4_mul(combs[kj], r)};
     hh::Aff<hh::Fq> ap[2];
     hh::jac_batch_affine(jp, ap, 2);
     uint8_t* u = u_out + i * HBH_G1_BYTES;

@@ -144,6 +144,15 @@ class Engine:
                                              ctypes.cast(out, ctypes.c_void_p)))
         return bytes(out)[:n]
 
+    def verify_ciphertexts_bp(self, u, w, qbp):
+        """Ciphertext::verify batch from hoststage.hash_g1_g2_bp points: e(G1K, W) == e(U, Q), the
+        reference's e(g1, W) == e(U, [KCOF] Q) by bilinearity (include/hbbft_hip.h hbh_hash_g1_g2_bp)."""
+        from . import hoststage
+        n = len(u)
+        if not n:
+            return b""
+        return self.verify_pairing_eq([hoststage.hash_bp_g1()] * n, w, None, u, qbp, None)
+
     def verify_pairing_eq_dev(self, stream, n, d_p1, d_q1, nq1, d_i1, d_p2, d_q2, nq2, d_i2, d_v):
         """Device-pointer variant (ints are raw device addresses, e.g. torch ``data_ptr()``);
         d_p1 / d_p2 = None means the G1 generator for every item."""

@@ -59,6 +59,35 @@ def hash_g1_g2(us, vs, threads=0):
     return _split(bytes(o), G2_BYTES, n)
 
 
+def hash_g1_g2_bp(us, vs, threads=0):
+    """Q_i with hash_g1_g2(U_i, V_i) = [KCOF] Q_i (hbh_hash_g1_g2_bp): Ciphertext::verify is then
+    e(hash_bp_g1(), W) == e(U, Q) (hbh_verify_pairing_eq), one G2 scalar multiplication less per
+    ciphertext than hash_g1_g2."""
+    l = _lib.lib()
+    n = len(us)
+    if len(vs) != n:
+        raise ValueError("us / vs length mismatch")
+    data, offs = _concat(vs)
+    ku, pu = _buf(b"".join(bytes(u) for u in us))
+    kd, pd = _buf(data)
+    o, po = _out(n * G2_BYTES)
+    check_host(l.hbh_hash_g1_g2_bp(n, pu, pd, offs.ctypes.data_as(ctypes.c_void_p), po, int(threads)))
+    return _split(bytes(o), G2_BYTES, n)
+
+
+_BP_G1 = None
+
+
+def hash_bp_g1():
+    """G1K = [KCOF^-1 mod r] g1, the P1 of the Q-form Ciphertext::verify (hbh_hash_bp_g1)."""
+    global _BP_G1
+    if _BP_G1 is None:
+        o, po = _out(G1_BYTES)
+        check_host(_lib.lib().hbh_hash_bp_g1(po))
+        _BP_G1 = bytes(o)
+    return _BP_G1
+
+
 def xor_with_hash(gs, datas, threads=0):
     """V xor stream(g) per item (PublicKeySet::decrypt's last step, SecretKey::decrypt)."""
     l = _lib.lib()

@@ -212,8 +212,10 @@ def _decrypt_batch(engine, sec_key, cts, threads=0):
     (sync_key_gen.rs:503-506, 535-538)."""
     if not cts:
         return []
-    huv = hoststage.hash_g1_g2([c.u for c in cts], [c.v for c in cts], threads)
-    ok = engine.verify_ciphertexts([c.u for c in cts], [c.w for c in cts], huv)
+    # Ciphertext::verify in its Q form (hbh_hash_g1_g2_bp): the same verdicts without the final
+    # G2 scalar multiplication of each hash
+    qbp = hoststage.hash_g1_g2_bp([c.u for c in cts], [c.v for c in cts], threads)
+    ok = engine.verify_ciphertexts_bp([c.u for c in cts], [c.w for c in cts], qbp)
     good = [k for k, v in enumerate(ok) if v]
     out = [None] * len(cts)
     if good:

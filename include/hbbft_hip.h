@@ -288,6 +288,15 @@ int hbh_hash_g1_g2(size_t n, const uint8_t* u, const uint8_t* data, const size_t
                    int threads);
 int hbh_xor_with_hash(size_t n, const uint8_t* g, const uint8_t* data, const size_t* offsets, uint8_t* out,
                       int threads);
+/* Ciphertext::verify without the last scalar multiplication of hash_g1_g2 (round 5): out[i] = Q_i,
+ * a G2 point with hash_g1_g2(U_i, V_i) = [KCOF] Q_i for one fixed scalar KCOF (G2::rand's cofactor
+ * multiplication h2 (x, y) = [KCOF] Q, Q = the Budroni-Pintore image of (x, y)).  By
+ * bilinearity Ciphertext::verify(U, V, W) = e(g1, W) == e(U, [KCOF] Q) = e(G1K, W) == e(U, Q) with
+ * G1K = [KCOF^-1 mod r] g1 (hbh_hash_bp_g1): hbh_verify_pairing_eq(P1 = G1K, Q1 = W, P2 = U, Q2 = Q)
+ * gives the reference's verdict bit for bit (SecretKey::decrypt, sync_key_gen.rs:503-506, 535-538). */
+int hbh_hash_g1_g2_bp(size_t n, const uint8_t* u, const uint8_t* data, const size_t* offsets, uint8_t* out,
+                      int threads);
+int hbh_hash_bp_g1(uint8_t* out);
 int hbh_signature_parity(size_t n, const uint8_t* sigs, uint8_t* out);
 int hbh_g1_compress(size_t n, const uint8_t* pts, uint8_t* out);
 int hbh_g2_compress(size_t n, const uint8_t* pts, uint8_t* out);

@@ -255,6 +255,11 @@ def test_encrypt_decrypt_batches_match_oracle(engine):
            Ciphertext(cts[2].u, cts[7].v, cts[7].w)]
     for c in bad:
         assert not tc.ciphertext_verify((_pt1(c.u), c.v, _pt2(c.w)))
+    # the Q-form check (hash_g1_g2_bp + e(G1K, W) == e(U, Q)) gives Ciphertext::verify's verdicts
+    us, vs, ws = [c.u for c in cts + bad], [c.v for c in cts + bad], [c.w for c in cts + bad]
+    want = bytes([1] * len(cts) + [0] * len(bad))
+    assert engine.verify_ciphertexts(us, ws, hoststage.hash_g1_g2(us, vs)) == want
+    assert engine.verify_ciphertexts_bp(us, ws, hoststage.hash_g1_g2_bp(us, vs)) == want
     plain = _decrypt_batch(engine, sk, cts + bad, threads=4)
     assert plain[:len(msgs)] == msgs
     assert plain[len(msgs):] == [None] * len(bad)

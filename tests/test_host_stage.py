@@ -157,6 +157,38 @@ def test_encrypt_matches_oracle(hs):
         assert hs.xor_with_hash([g], [v])[0] == m
 
 
+def test_encrypt_key_combs_equal_glv(hs):
+    """hbh_encrypt builds a 4-bit comb for a key that encrypts >= 16 items of one call (SyncKeyGen's
+    Acks: N values per key) and uses GLV otherwise: 2 x 20 items to two keys in one call equal the
+    same items encrypted one call each, and the oracle on a sample."""
+    rng = random.Random(41)
+    sks = [rng.randrange(1, C.R) for _ in range(2)]
+    pks = [C.g1_mul(C.G1_GEN, k) for k in sks]
+    msgs = [bytes(rng.randrange(256) for _ in range(rng.choice([32, 100]))) for _ in range(40)]
+    rs = [rng.randrange(1, C.R) for _ in msgs] + [0, C.R - 1]
+    msgs += [b"x", b"y"]
+    keys = [abi_g1(pks[i % 2]) for i in range(len(msgs))]
+    got = hs.encrypt(keys, msgs, rs, threads=2)
+    assert got == [hs.encrypt([k], [m], [r])[0] for k, m, r in zip(keys, msgs, rs)]
+    for i in (0, 7, 40):
+        eu, ev, ew = tc.encrypt(pks[i % 2], msgs[i], rs[i])
+        assert got[i] == (abi_g1(eu), ev, abi_g2(ew))
+
+
+def test_hash_bp_form(hs):
+    """Q-form Ciphertext::verify inputs: [KCOF] hash_g1_g2_bp(U, V) == hash_g1_g2(U, V) and
+    hash_bp_g1() == [KCOF^-1] g1, with KCOF = h2 s^-1 mod r from its definition."""
+    z, lam = -C.X_ABS, C.P % C.R
+    s_ = ((z * z - z - 1) + (z - 1) * lam + 2 * lam * lam) % C.R
+    kcof = C.H2 * pow(s_, -1, C.R) % C.R
+    rng = random.Random(12)
+    us = [abi_g1(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) for _ in range(6)]
+    vs = [bytes(rng.randrange(256) for _ in range(ln)) for ln in (0, 32, 64, 65, 200, 1096)]
+    q = hs.hash_g1_g2_bp(us, vs, threads=2)
+    assert hs.g2_mul(q, [kcof] * len(q)) == hs.hash_g1_g2(us, vs)
+    assert hs.hash_bp_g1() == abi_g1(C.g1_mul(C.G1_GEN, pow(kcof, -1, C.R)))
+
+
 def test_bad_arguments(hs):
     from hbbft_amd._lib import HbhError
     with pytest.raises(HbhError):
