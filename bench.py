@@ -984,6 +984,9 @@ def dkg_node_round(eng, n_nodes, t, seed=5):
     acks = [(y - 1, Ack(p, [Ciphertext(*val_cts[p * n_nodes + y - 1])] * n_nodes))
             for p in range(n_nodes) for y in ys]
     out = {}
+    # one untimed Part first: the process's one-time lazy set-up (host comb tables, engine tables,
+    # kernel modules) is not part of a node's round
+    SyncKeyGen.new(our, sks[our], pks, t, eng, rng=random.Random(seed + 3), threads=threads)
     t0 = time.perf_counter()
     _, own_part = SyncKeyGen.new(our, sks[our], pks, t, eng, rng=random.Random(seed + 1), threads=threads)
     out["generate_part_ms"] = (time.perf_counter() - t0) * 1e3

@@ -72,7 +72,35 @@ class BinaryAgreementCoin:
         return False, None, ts
 
     # ------------------------------------------------------------ messages (:245-266)
+    def handle_fast(self, sender, epoch, share):
+        """The outcomes most coin messages have, without building Steps: True when handle_message's
+        result would be an empty Step and its state change is done here -- ignored (decided, an
+        expired epoch, a coin already decided or pending), a future epoch's first share from this
+        sender stored in the incoming queue, or a current-epoch share stored by
+        ThresholdSign.store_cached.  False: nothing changed (a fault, the share that completes the
+        coin, an uncached verdict, or the verifier's shortcuts off) -- call handle_message."""
+        if not getattr(self.verifier, "shortcuts", False):
+            return False
+        if self.decision is not None or epoch < self.epoch:
+            return True
+        if epoch > self.epoch:
+            if epoch > self.epoch + self.max_future_epochs or type(share) is not bytes:
+                return False
+            q = self.incoming.get(epoch)
+            if q is None:
+                q = self.incoming[epoch] = {}
+            elif sender in q:
+                return False
+            q[sender] = share
+            self.queued += 1
+            return True
+        if self.coin_decided or self.pending is not None:
+            return True
+        return self.ts.store_cached(sender, share)
+
     def handle_message(self, sender, epoch, share):
+        if self.handle_fast(sender, epoch, share):
+            return Step()
         if self.decision is not None or epoch < self.epoch:  # Coin messages can expire
             return Step()
         if epoch > self.epoch + self.max_future_epochs:
@@ -95,23 +123,6 @@ class BinaryAgreementCoin:
         except ProtocolError as e:  # Error::HandleThresholdSign
             raise ProtocolError("HandleThresholdSign", e.kind)
         return self._on_coin_step(ts_step)
-
-    def _store_valid_share(self, sender, share):
-        """_handle_coin's most common outcome without its call chain and empty Steps: a share with a
-        cached valid verdict from a new sender that leaves the coin below t + 1 shares is stored in
-        the ThresholdSign (threshold_sign.rs:181-197).  False: nothing done, take the full path."""
-        if self.coin_decided or self.pending is not None:
-            return False
-        ts, ni = self.ts, self.netinfo
-        rs, h = ts.received_shares, ts.doc_hash
-        if ts.terminated or h is None or sender in rs or len(rs) >= ni.t or type(share) is not bytes:
-            return False
-        idx, pk, d = ni._index.get(sender), ni.pk_shares.get(sender), self.verifier._sig.get(h)
-        if idx is None or type(pk) is not bytes or d is None or d.get((pk, share)) is not True:
-            return False
-        self.verifier.lookups += 1
-        rs[sender] = (idx, share)
-        return True
 
     def _on_coin_step(self, ts_step):  # :394-405
         epoch = self.epoch
@@ -210,7 +221,7 @@ class BinaryAgreementCoin:
             if queued:
                 self.verifier.drain()
         for sender, share in replay:
-            if self._store_valid_share(sender, share):
+            if not self.coin_decided and self.pending is None and self.ts.store_cached(sender, share):
                 continue
             step.extend(self._handle_coin(sender, share))
             if self.decision is not None:

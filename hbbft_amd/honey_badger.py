@@ -352,7 +352,7 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
 
 def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
               defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True, preverify_at="first_drain",
-              after_prep=None):
+              after_prep=None, fast_paths=True):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
     ``slack``: shares pre-verified per instance beyond the t + 1 it needs (None: every share).
@@ -372,7 +372,10 @@ def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=Fals
     not share the host threads with the prep.
     ``ba``: the coins come from Binary Agreement instances (``trace.with_ba``; default: when the
     trace has a BA side) -- hbbft_amd.binary_agreement's epochs, fixed coins and future-epoch queue,
-    our SBV / Conf outcomes released along the message stream, coin combines deferred per window."""
+    our SBV / Conf outcomes released along the message stream, coin combines deferred per window.
+    ``fast_paths``: the instances' cached-verdict transitions (ThresholdSign / ThresholdDecrypt
+    ``store_cached``, BinaryAgreementCoin ``handle_fast``); False sends every message through the full
+    ``handle_message`` path (tests/test_gpu_honey_badger.py compares the two)."""
     if ba is None:
         ba = getattr(trace, "ba", None) is not None
     old = sys.getswitchinterval()
@@ -380,7 +383,7 @@ def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=Fals
         sys.setswitchinterval(switch_interval)
     try:
         return _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch,
-                          preverify, preverify_at, after_prep)
+                          preverify, preverify_at, after_prep, fast_paths)
     finally:
         sys.setswitchinterval(old)
 
@@ -518,7 +521,7 @@ def _one_call(engine2, jobs):
 
 
 def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None,
-               preverify=True, preverify_at="first_drain", after_prep=None):
+               preverify=True, preverify_at="first_drain", after_prep=None, fast_paths=True):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     # the background host work leaves two of the host threads to the flows and the drain worker
@@ -531,6 +534,7 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
             prep.add_done_callback(lambda _f: after_prep())
     ver = BatchVerifier(engine, combine_engine(engine) if pipelined and hasattr(engine, "device") else None)
     ver.recording = defer                  # combines of the epoch run in one batch at the end
+    ver.shortcuts = fast_paths
     pre_box = []  # the pre-verification future, once started
 
     def start_preverify():
@@ -646,7 +650,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                     except ProtocolError as err:
                         res.errors.append(("coin", p, err))
 
-    sig_cache, ni_index, ni_pks, ni_t = ver._sig, ni._index, ni.pk_shares, ni.t
+    sig_cache = ver._sig
 
     pks = keys.pks
 
@@ -676,39 +680,10 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
         for m in batch:
             p, e, j = m
             b = bas[p]
-            # a decided instance ignores every message (:245-248); an expired epoch's coin message and
-            # a share for a coin already decided or pending are empty Steps (:250-252, _handle_coin):
-            # skipped here without building them
-            be = b.epoch
-            if b.decision is not None or e < be or (e == be and (b.coin_decided or b.pending is not None)):
+            # the common outcomes (ignored, future share queued, cached valid share stored) inside
+            # BinaryAgreementCoin.handle_fast; everything else through handle_message
+            if b.handle_fast(j, e, shares[m]):
                 continue
-            # The two outcomes most messages have, as BinaryAgreementCoin.handle_message would reach
-            # them, without its call chain and empty Steps: a future epoch's share stored in the
-            # incoming queue (first from this sender), and a current-epoch share with a cached valid
-            # verdict that leaves the coin below t + 1 shares.  Everything else (faults, a share that
-            # completes the coin, a verdict not cached) takes the full path below.
-            share = shares[m]
-            if e > be:
-                if e <= be + b.max_future_epochs:
-                    q = b.incoming.get(e)
-                    if q is None:
-                        q = b.incoming[e] = {}
-                    if j not in q and type(share) is bytes:
-                        q[j] = share
-                        b.queued += 1
-                        continue
-            else:
-                ts = b.ts
-                rs = ts.received_shares
-                h = ts.doc_hash
-                if not ts.terminated and h is not None and j not in rs and len(rs) < ni_t:
-                    idx, pk = ni_index.get(j), ni_pks.get(j)
-                    d = sig_cache.get(h)
-                    if (idx is not None and type(pk) is bytes and type(share) is bytes and d is not None
-                            and d.get((pk, share)) is True):
-                        ver.lookups += 1
-                        rs[j] = (idx, share)
-                        continue
             try:
                 step = b.handle_message(j, e, ba.shares[m])
             except ProtocolError as err:
@@ -866,7 +841,7 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
 
     handed_dec = {p: handed.setdefault(("dec", p), []) for p in td}
 
-    dec_cache, dni_index, dni_pks, dni_t = ver._dec, ni_dec._index, ni_dec.pk_shares, ni_dec.t
+    dec_cache = ver._dec
 
     def hand_dec(p, j):
         handed_dec[p].append(j)
@@ -874,15 +849,9 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
         if inst.terminated:  # handle_message of a terminated instance is an empty Step (:183-185)
             return _EMPTY
         share = dec_sh[(p, j)]
-        # the outcome most shares have, as ThresholdDecrypt.handle_message would reach it: a cached
-        # valid verdict from a new sender that leaves the instance below t + 1 shares (the rest, full path)
-        ct, sh = inst.ciphertext, inst.shares
-        if ct is not None and j not in sh and len(sh) < dni_t and type(share) is bytes:
-            idx, pk, d = dni_index.get(j), dni_pks.get(j), dec_cache.get((ct.huv, ct.w))
-            if idx is not None and type(pk) is bytes and d is not None and d.get((pk, share)) is True:
-                ver.lookups += 1
-                sh[j] = (idx, share)
-                return _EMPTY
+        # the outcome most shares have (ThresholdDecrypt.store_cached), else the full path
+        if inst.store_cached(j, share):
+            return _EMPTY
         return inst.handle_message(j, share)
 
     dec_msgs = [m for m in trace.dec_msgs if m[0] in td]  # (shares of a faulted contribution: no instance)

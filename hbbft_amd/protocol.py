@@ -146,6 +146,10 @@ class BatchVerifier:
         self.max_batch = 0
         self.recording = False  # deferred mode: combines return Deferred, run later in one batch
         self.lookups = 0        # verdicts the flows consumed (the checks the reference performs)
+        # the instances' store_cached / handle_fast transitions (one copy each, inside ThresholdSign,
+        # ThresholdDecrypt and BinaryAgreementCoin); False routes every message through the full
+        # handle_message path (run_epoch(fast_paths=False): the equivalence tests)
+        self.shortcuts = True
         self._docs = {}
         self._rec_g2, self._rec_g1 = [], []
         self._released = set()  # instances released since the last drain was stored
@@ -524,8 +528,26 @@ class ThresholdSign:
         step.messages.append(("all", share))
         return step.extend(self.handle_message(self.netinfo.our_id, share))
 
+    def store_cached(self, sender_id, share):
+        """handle_message's most common transition without building its Step (:181-197): the document
+        is set, the sender is new, the verifier already holds a VALID verdict for the share, and
+        storing it leaves the instance at <= t shares -- the share is stored, True is returned, and
+        handle_message's result would have been an empty Step.  Otherwise (or with the verifier's
+        shortcuts off) nothing changes and False is returned: handle_message decides."""
+        ni, rs, h = self.netinfo, self.received_shares, self.doc_hash
+        if (self.terminated or h is None or sender_id in rs or len(rs) >= ni.t or type(share) is not bytes
+                or not getattr(self.verifier, "shortcuts", False)):
+            return False
+        idx, pk = ni._index.get(sender_id), ni.pk_shares.get(sender_id)
+        d = self.verifier._sig.get(h)
+        if idx is None or type(pk) is not bytes or d is None or d.get((pk, share)) is not True:
+            return False
+        self.verifier.lookups += 1  # the verdict consumed, as sig_valid counts it
+        rs[sender_id] = (idx, share)
+        return True
+
     def handle_message(self, sender_id, share):  # :181-197
-        if self.terminated:
+        if self.terminated or self.store_cached(sender_id, share):
             return Step()
         ni = self.netinfo
         idx = ni._index.get(sender_id)  # node_index
@@ -654,8 +676,26 @@ class ThresholdDecrypt:
         step.messages.append(("all", share))
         return step.join(self.try_output())
 
+    def store_cached(self, sender_id, share):
+        """handle_message's most common transition without building its Step (:182-201): the
+        ciphertext is set, the sender is new (no MultipleDecryptionShares), the verifier already holds
+        a VALID verdict for the share, and storing it leaves the instance at <= t shares -- stored,
+        True returned (handle_message would return an empty Step).  Otherwise (or with the verifier's
+        shortcuts off) nothing changes and False is returned: handle_message decides."""
+        ni, sh, ct = self.netinfo, self.shares, self.ciphertext
+        if (self.terminated or ct is None or sender_id in sh or len(sh) >= ni.t or type(share) is not bytes
+                or not getattr(self.verifier, "shortcuts", False)):
+            return False
+        idx, pk = ni._index.get(sender_id), ni.pk_shares.get(sender_id)
+        d = self.verifier._dec.get((ct.huv, ct.w))
+        if idx is None or type(pk) is not bytes or d is None or d.get((pk, share)) is not True:
+            return False
+        self.verifier.lookups += 1  # the verdict consumed, as dec_valid counts it
+        sh[sender_id] = (idx, share)
+        return True
+
     def handle_message(self, sender_id, share):  # :182-201
-        if self.terminated:
+        if self.terminated or self.store_cached(sender_id, share):
             return Step()
         ni = self.netinfo
         idx = ni._index.get(sender_id)  # node_index
