@@ -229,3 +229,54 @@ def test_preverify_one_call_matches_separate_calls(engine):
     separate = {kind: (keys_, v) for kind, keys_, v in BatchVerifier(engine)._run_jobs(jobs)}
     assert merged == separate
     assert 0 < sum(separate["ct"][1]) < len(ps) and 0 < sum(separate["dec"][1]) < len(separate["dec"][0])
+
+
+def _outcome(r):
+    """Everything an epoch's Steps determine, faults and errors in order."""
+    return (r.ba_decisions, r.ba_coins, r.coins, r.signatures, r.plaintexts,
+            [(k, p, f.node_id, f.kind) for k, p, f in r.faults], [(k, p, e.kind, e.detail) for k, p, e in r.errors])
+
+
+@pytest.mark.parametrize("adversary", ["random", "faulty_share"])
+def test_epoch_fast_paths_equal_full_path_n100(engine, adversary):
+    """configs[4] at N=100, f=33 with BA coins and the Random / FaultyShare adversaries of
+    tests/honey_badger.rs:26-245: the cached-verdict transitions (ThresholdSign / ThresholdDecrypt
+    .store_cached, BinaryAgreementCoin.handle_fast; threshold_sign.rs:181-197, threshold_decrypt.rs:
+    182-201, binary_agreement.rs:245-264) give the same decisions, coins, signatures, plaintexts,
+    faults (in order) and errors as every message through handle_message (fast_paths=False)."""
+    rng = random.Random({"random": 5100, "faulty_share": 5101}[adversary])
+    keys = NetworkKeys(engine, 100, 33, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=1, bad_every=41, proposal_bytes=200, n_adv=33,
+                                adversary=adversary, inject=0.3)
+    trace.with_ba(engine, rng, extra=0.2, bad_every=43)
+    fast = run_epoch(engine, keys, trace)
+    full = run_epoch(engine, keys, trace, fast_paths=False)
+    assert _outcome(fast) == _outcome(full)
+    assert fast.plaintexts == trace.proposals and fast.errors == []
+    assert fast.ba_decisions == trace.ba.decision and fast.ba_coins == trace.ba.coins
+    assert fast.faults and all(f.node_id in trace.adv or (k, p, f.node_id) in (trace.bad | trace.ba.bad)
+                               for k, p, f in fast.faults)
+
+
+@pytest.mark.parametrize("n", [7, 13])
+def test_ba_epoch_pipelined_and_prefetch_equal_serial(engine, n):
+    """the pipelined BA coin phase (windows 1 and 3) and the prefetched coin documents
+    (prefetch_coins: hashes and our shares computed before the epoch) give the serial run's Steps
+    at the same window: decisions, coins, plaintexts and the full fault list (kind, proposer,
+    sender, fault kind) in order; fast paths off gives them too."""
+    from hbbft_amd.honey_badger import prefetch_coins
+    t = (n - 1) // 3
+    rng = random.Random(900 + n)
+    keys = NetworkKeys(engine, n, t, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=4, bad_every=7, proposal_bytes=48)
+    trace.with_ba(engine, rng, extra=0.4, bad_every=7)
+    for w in (1, 3):
+        serial = run_epoch(engine, keys, trace, window=w, pipelined=False)
+        assert serial.ba_decisions == trace.ba.decision and serial.plaintexts == trace.proposals
+        pip = run_epoch(engine, keys, trace, window=w, pipelined=True)
+        pre = run_epoch(engine, keys, trace, window=w, pipelined=True,
+                        coin_prefetch=prefetch_coins(keys, trace.hb_epoch, range(n)))
+        full = run_epoch(engine, keys, trace, window=w, pipelined=False, fast_paths=False)
+        assert _outcome(pip) == _outcome(serial)
+        assert _outcome(pre) == _outcome(serial)
+        assert _outcome(full) == _outcome(serial)
