@@ -461,7 +461,7 @@ def main():
                          "epochs/s; 8,192: 18.5-19.4; 4,096: 8 calls, 15.9-18.9; profiles/r04/c27_*, c28_*)")
     ap.add_argument("--epoch-coins", choices=["ba", "synthetic"], default="ba",
                     help="epoch workload: coins from Binary Agreement instances or one ThresholdSign each")
-    ap.add_argument("--ack-impl", choices=["auto", "quad", "lane"], default="auto",
+    ap.add_argument("--ack-impl", choices=["auto", "quad", "lane", "horner"], default="auto",
                     help="dkg workload: Ack-check kernel (hbh_engine_set_ack_impl)")
     ap.add_argument("--dkg-nodes", type=int, default=0,
                     help="dkg workload, network scope: checking nodes (0 = all 100; 10,000 acks each)")
@@ -819,7 +819,7 @@ def run_dkg(args, eng, world, rank, dev):
         nodes = [x for x in range(1, (args.dkg_nodes or n_nodes) + 1) if (x - 1) % world == rank]
     else:
         nodes = [rank + 1]
-    eng.set_ack_impl({"auto": 0, "quad": 1, "lane": 2}[args.ack_impl])
+    eng.set_ack_impl({"auto": 0, "quad": 1, "lane": 2, "horner": 3}[args.ack_impl])
     t0 = time.perf_counter()
     commits, pidx, xs, ys, vals, expected = dkg_workload(eng, 100, n_nodes, t, nodes)
     gen_s = time.perf_counter() - t0
@@ -879,10 +879,16 @@ def run_dkg(args, eng, world, rank, dev):
     for part in gather_per_rank({int(x): vb[xa == x].tobytes() for x in nodes}, world):
         by_node.update(part)
     if rank == 0:
-        ops = [workcount.bivar_ack(t, y) for y in range(1, n_nodes + 1)]
-        op = (sum(o[0] for o in ops) / n_nodes, sum(o[1] for o in ops) / n_nodes)
-        lane = args.ack_impl == "lane" or (args.ack_impl == "auto" and nack >= ACK_LANE_MIN)
-        kname = "hb::k_bivar_check" if lane else "hbs::k_bivar_check_quad"
+        lane = args.ack_impl in ("lane", "horner") or (args.ack_impl == "auto" and nack >= ACK_LANE_MIN)
+        fd = lane and args.ack_impl != "horner"
+        if fd:   # every row (part, x) holds the acks of all senders y = 1..N: one dense run
+            row = workcount.bivar_row_fd(t, 1, n_nodes, n_nodes)
+            op = (row[0] / n_nodes, row[1] / n_nodes)
+        else:
+            ops = [workcount.bivar_ack(t, y) for y in range(1, n_nodes + 1)]
+            op = (sum(o[0] for o in ops) / n_nodes, sum(o[1] for o in ops) / n_nodes)
+        kname = ("hb::k_bivar_fd_horner + k_bivar_fd_run + k_bivar_fd_check" if fd else
+                 "hb::k_bivar_check" if lane else "hbs::k_bivar_check_quad")
         waves = (1 if lane else 4) * nack / 64 / 1024
         main_k = roofline_entry(kname, dev_n, dev_ms, nack, op, "ack check", waves)
         line = {
@@ -908,6 +914,8 @@ def run_dkg(args, eng, world, rank, dev):
             "verdicts_sha256": hashlib.sha256(b"".join(by_node[x] for x in sorted(by_node))).hexdigest(),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)",
                              note="%s; %.1f waves per SIMD launched" % (
+                                 "finite differences over each row's dense y run (Horner at t + 1 points, t "
+                                 "additions per further y; per-ack work = the row's work / its acks)" if fd else
                                  "one lane per ack on affine rows" if lane else "four lanes per ack (lane quads)",
                                  waves)),
             "ack_impl": kname,

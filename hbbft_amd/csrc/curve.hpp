@@ -156,6 +156,13 @@ HB_HD Jac<F> jac_mul_small(const Jac<F>& p, uint32_t k) {
   return acc;
 }
 
+template <class F>
+HB_HD Jac<F> jac_neg(const Jac<F>& p) {
+  Jac<F> r = p;
+  r.y = fneg(p.y);
+  return r;
+}
+
 // P == Q as group elements (cross-multiplied Jacobian coordinates)
 template <class F>
 HB_HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {

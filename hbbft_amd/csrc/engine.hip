@@ -130,6 +130,9 @@ struct hbh_engine {
   uint8_t* h_stage = nullptr;  // pinned host staging of the split check (one upload, one download)
   size_t h_stage_cap = 0;
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
+  // Ack checks of dense y runs by finite differences (hbl::bivar_fd); HBH_ACK_FD=0: Horner only (A/B)
+  bool ack_fd = true;
+  DevBuf fd_e, fd_meta;
   size_t split_max = 0;  // HBH_SPLIT_MAX: most combines per call on the split check (0: the wave rule)
   // commitment sets created on this engine: hbh_engine_destroy frees their device memory and
   // detaches them, so a set destroyed after its engine never touches the freed engine
@@ -343,6 +346,7 @@ int hbh_engine_create(int device, hbh_engine** out) {
   hbh_engine* e = new hbh_engine();
   e->device = device;
   if (const char* v = std::getenv("HBH_SPLIT_CHECK")) e->split_check = std::atoi(v) != 0;
+  if (const char* v = std::getenv("HBH_ACK_FD")) e->ack_fd = std::atoi(v) != 0;
   if (const char* v = std::getenv("HBH_SPLIT_MAX")) e->split_max = (size_t)std::max(0, std::atoi(v));
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (err == hipSuccess) err = hipEventCreateWithFlags(&e->done, hipEventDisableTiming);
@@ -379,7 +383,7 @@ int hbh_engine_destroy(hbh_engine* e) {
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
                     &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval, &e->split_in,
-                    &e->split_out})
+                    &e->split_out, &e->fd_e, &e->fd_meta})
     b->release();
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   (void)hipEventDestroy(e->done);
@@ -493,7 +497,7 @@ int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
 
 int hbh_engine_set_ack_impl(hbh_engine* e, int impl) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
-  if (impl != HBH_ACK_AUTO && impl != HBH_ACK_QUAD && impl != HBH_ACK_LANE)
+  if (impl != HBH_ACK_AUTO && impl != HBH_ACK_QUAD && impl != HBH_ACK_LANE && impl != HBH_ACK_LANE_HORNER)
     return fail(HBH_ERR_ARG, "unknown Ack-check implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->ack_impl = impl;
@@ -1572,6 +1576,60 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, bool affine, size_t n, const uin
   return HBH_OK;
 }
 
+// Finite-difference plan of an Ack drain (hbl::bivar_fd): a row slot whose acks form a dense run of y
+// -- at least 2 (t + 1) acks spanning at most twice as many consecutive y, as a node's drain has (one
+// Ack per sender per Part) -- is evaluated at every y of its span by t + 1 Horner points and t
+// additions per further y; its acks then compare against those points (epos).  Every other ack takes
+// the Horner kernel (other, in order of y).  FD rows are sorted by span length (the run kernel's
+// workgroups step their rows together).
+struct FdPlan {
+  std::vector<uint32_t> slot, y0, off, len;  // per FD row
+  std::vector<uint32_t> epos;                // per ack (FD acks only)
+  std::vector<uint32_t> fd_acks, other;      // ack lists
+  size_t npts = 0;                           // E points of all FD rows
+};
+void plan_fd(size_t n, const std::vector<uint32_t>& slot, const uint32_t* ys, int t, FdPlan& P) {
+  const uint64_t T1 = (uint64_t)t + 1;
+  uint32_t nslot = 0;
+  for (size_t a = 0; a < n; a++) nslot = std::max(nslot, slot[a] + 1);
+  std::vector<uint32_t> cnt(nslot, 0), ymin(nslot, 0xffffffffu), ymax(nslot, 0);
+  for (size_t a = 0; a < n; a++) {
+    const uint32_t s = slot[a];
+    cnt[s]++;
+    ymin[s] = std::min(ymin[s], ys[a]);
+    ymax[s] = std::max(ymax[s], ys[a]);
+  }
+  std::vector<uint32_t> cand;
+  for (uint32_t s = 0; s < nslot; s++) {
+    if (!cnt[s] || T1 > 128) continue;
+    const uint64_t span = (uint64_t)ymax[s] - ymin[s] + 1;
+    if (cnt[s] >= 2 * T1 && span <= 2 * (uint64_t)cnt[s] && span > T1 && span < ((uint64_t)1 << 20)) cand.push_back(s);
+  }
+  std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) {
+    const uint32_t la = ymax[a] - ymin[a], lb = ymax[b] - ymin[b];
+    return la != lb ? la > lb : ymin[a] < ymin[b];
+  });
+  std::vector<int32_t> fd_of(nslot, -1);
+  for (uint32_t s : cand) {
+    fd_of[s] = (int32_t)P.slot.size();
+    P.slot.push_back(s);
+    P.y0.push_back(ymin[s]);
+    P.off.push_back((uint32_t)P.npts);
+    P.len.push_back(ymax[s] - ymin[s] + 1);
+    P.npts += ymax[s] - ymin[s] + 1;
+  }
+  P.epos.assign(n, 0);
+  for (size_t a = 0; a < n; a++) {
+    const int32_t f = fd_of[slot[a]];
+    if (f < 0) {
+      P.other.push_back((uint32_t)a);
+    } else {
+      P.epos[a] = P.off[f] + (ys[a] - P.y0[f]);
+      P.fd_acks.push_back((uint32_t)a);
+    }
+  }
+}
+
 // Acks in order of y (stable): the lanes of a wave then run the same small-scalar double-and-add.
 // y is a node index + 1, so a counting sort does it in O(n) (10^6 acks of a network-wide check).
 // Round 4 measured (row tile, y) orders, whose waves re-read one tile's rows while they sit in L2:
@@ -1715,11 +1773,22 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
   if (rc) return rc;
   // lane quads (four lanes per ack, one wave per SIMD) for latency; one lane per ack on affine
   // rows (two waves per SIMD, mixed additions) for throughput
-  const bool lane = e->ack_impl == HBH_ACK_LANE || (e->ack_impl == HBH_ACK_AUTO && nack >= HBH_ACK_LANE_MIN);
+  const bool lane = e->ack_impl == HBH_ACK_LANE || e->ack_impl == HBH_ACK_LANE_HORNER ||
+                    (e->ack_impl == HBH_ACK_AUTO && nack >= HBH_ACK_LANE_MIN);
   std::vector<uint32_t> slot;
   rc = set_rows(cs, s, lane, nack, part_idx, xs, slot);
   if (rc) return rc;
-  order_by_y(nack, ys, order);
+  FdPlan fd;
+  if (lane && e->ack_fd && e->ack_impl != HBH_ACK_LANE_HORNER) {
+    plan_fd(nack, slot, ys, t, fd);
+    // the Horner kernel's acks in order of y
+    std::vector<uint32_t> oy(fd.other.size());
+    for (size_t k = 0; k < fd.other.size(); k++) oy[k] = ys[fd.other[k]];
+    order_by_y(fd.other.size(), oy.data(), order);
+    for (auto& o : order) o = fd.other[o];
+  } else {
+    order_by_y(nack, ys, order);
+  }
   HBH_CHECK(e->in_b.ensure(nack * 12));
   HBH_CHECK(e->in_c.ensure(nack * HBH_FR_BYTES));
   HBH_CHECK(e->out_v.ensure(nack));
@@ -1728,14 +1797,35 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
   uint32_t* d_ord = d_y + nack;
   HBH_CHECK(hipMemcpyAsync(d_ro, slot.data(), nack * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(d_y, ys, nack * 4, hipMemcpyHostToDevice, s));
-  HBH_CHECK(hipMemcpyAsync(d_ord, order.data(), nack * 4, hipMemcpyHostToDevice, s));
+  if (!order.empty()) HBH_CHECK(hipMemcpyAsync(d_ord, order.data(), order.size() * 4, hipMemcpyHostToDevice, s));
   HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
+  const size_t nfd = fd.slot.size();
+  uint32_t* d_fd = nullptr;
+  if (nfd) {
+    const size_t words = 4 * nfd + 2 * nack;
+    HBH_CHECK(e->fd_meta.ensure(words * 4));
+    HBH_CHECK(e->fd_e.ensure(fd.npts * hbl::fd_point_bytes()));
+    d_fd = (uint32_t*)e->fd_meta.p;
+    HBH_CHECK(hipMemcpyAsync(d_fd, fd.slot.data(), nfd * 4, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipMemcpyAsync(d_fd + nfd, fd.y0.data(), nfd * 4, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipMemcpyAsync(d_fd + 2 * nfd, fd.off.data(), nfd * 4, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipMemcpyAsync(d_fd + 3 * nfd, fd.len.data(), nfd * 4, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipMemcpyAsync(d_fd + 4 * nfd, fd.epos.data(), nack * 4, hipMemcpyHostToDevice, s));
+    HBH_CHECK(hipMemcpyAsync(d_fd + 4 * nfd + nack, fd.fd_acks.data(), fd.fd_acks.size() * 4, hipMemcpyHostToDevice, s));
+  }
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  if (lane)
-    HBH_CHECK(hbl::bivar_check(s, (int)nack, t, cs->rows[1].p, d_ro, d_y, (const uint32_t*)e->in_c.p, e->fbtab.p,
-                               (uint8_t*)e->out_v.p, d_ord));
+  if (lane && nfd) {
+    HBH_CHECK(hbl::bivar_fd(s, (int)nfd, t, cs->rows[1].p, d_fd, d_fd + nfd, d_fd + 2 * nfd, d_fd + 3 * nfd,
+                            e->fd_e.p));
+    HBH_CHECK(hbl::bivar_fd_check(s, (int)fd.fd_acks.size(), e->fd_e.p, d_fd + 4 * nfd, (const uint32_t*)e->in_c.p,
+                                  e->fbtab.p, d_fd + 4 * nfd + nack, (uint8_t*)e->out_v.p));
+    HBH_CHECK(hbl::bivar_check(s, (int)order.size(), t, cs->rows[1].p, d_ro, d_y, (const uint32_t*)e->in_c.p,
+                               e->fbtab.p, (uint8_t*)e->out_v.p, d_ord));
+  } else if (lane)
+    HBH_CHECK(hbl::bivar_check(s, (int)order.size(), t, cs->rows[1].p, d_ro, d_y, (const uint32_t*)e->in_c.p,
+                               e->fbtab.p, (uint8_t*)e->out_v.p, d_ord));
   else
     HBH_CHECK(hbl::bivar_check_quad(s, (int)nack, t, cs->rows[0].p, d_ro, d_y, (const uint32_t*)e->in_c.p,
                                     e->fbtab.p, (uint8_t*)e->out_v.p, d_ord));

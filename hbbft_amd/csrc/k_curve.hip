@@ -488,6 +488,122 @@ __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint
   verdict[a] = jac_eq(acc, w) ? 1 : 0;
 }
 
+// ------------------------------------------------------------------ Ack checks by finite differences
+// The acks of one row R = row(x) (one Part, one checking node x) evaluate the same degree-t polynomial
+// E(y) = sum_j R_j y^j at the senders' y = 1..N.  For a dense run of y (a row with many acks, as every
+// node's Ack drain has: one Ack per sender per Part) E is evaluated at y0 .. y0 + L - 1 as
+//   1. Horner at the first t + 1 points (k_bivar_fd_horner, one lane per point),
+//   2. the forward-difference table D_k = Delta^k E(y0) of those points (t levels of subtractions),
+//   3. D_k += D_{k+1} (k < t) per step of y: every further E(y) costs t independent G1 additions
+//      instead of a Horner of t steps by a small scalar (k_bivar_fd_run: one lane per (row, k)),
+// and each ack compares its E(y) with g1 * val (k_bivar_fd_check).  Exact group arithmetic throughout:
+// the verdicts are the Horner kernel's bit for bit (tests/test_gpu_commit_set.py compares them).
+// E values are stored as Jacobian points (FD_WORDS words each).
+constexpr int FD_WORDS = 3 * NL;
+
+__device__ __forceinline__ void jac_store(uint32_t* __restrict__ w, const Jac<Fp>& p) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    w[i] = p.x.l[i];
+    w[NL + i] = p.y.l[i];
+    w[2 * NL + i] = p.z.l[i];
+  }
+}
+__device__ __forceinline__ Jac<Fp> jac_load(const uint32_t* __restrict__ w) {
+  Jac<Fp> p;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    p.x.l[i] = w[i];
+    p.y.l[i] = w[NL + i];
+    p.z.l[i] = w[2 * NL + i];
+  }
+  return p;
+}
+
+// E(y) = sum_j R_j y^j by Horner with the small y over an affine row
+__device__ __forceinline__ Jac<Fp> row_horner(const uint32_t* __restrict__ R, int t, uint32_t y) {
+  Jac<Fp> acc = jac_zero<Fp>();
+  for (int j = t; j >= 0; j--) {
+    acc = jac_mul_small(acc, y);
+    Fp rx, ry;
+    bool inf;
+    load_g1(R + (size_t)j * G1_WORDS, rx, ry, inf);
+    if (!inf) acc = jac_add_affine(acc, rx, ry);
+  }
+  return acc;
+}
+
+// step 1: lane g = i * nfd + f evaluates FD row f at y0[f] + i (i <= t); i-major, so the lanes of a
+// wave share i (and y, for rows of one y0: the small-scalar chains do not diverge)
+__global__ void __launch_bounds__(256) k_bivar_fd_horner(int nfd, int t, const uint32_t* __restrict__ rows,
+                                                         const uint32_t* __restrict__ fd_slot,
+                                                         const uint32_t* __restrict__ fd_y0,
+                                                         const uint32_t* __restrict__ fd_off, uint32_t* __restrict__ ebuf) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nfd * (t + 1)) return;
+  const int i = g / nfd, f = g % nfd;
+  const uint32_t* R = rows + (size_t)fd_slot[f] * (t + 1) * G1_WORDS;
+  jac_store(ebuf + ((size_t)fd_off[f] + i) * FD_WORDS, row_horner(R, t, fd_y0[f] + (uint32_t)i));
+}
+
+// steps 2-3: one workgroup per G = blockDim / (t + 1) FD rows, lane (r, k) holds D_k of row r; the
+// neighbour's D crosses lanes through LDS (blockDim x FD_WORDS words).  Rows are sorted by length, so
+// a workgroup's rows step together; a row stops at its own length.
+__global__ void __launch_bounds__(256) k_bivar_fd_run(int nfd, int t, const uint32_t* __restrict__ fd_off,
+                                                      const uint32_t* __restrict__ fd_len, uint32_t* __restrict__ ebuf) {
+  extern __shared__ uint32_t fd_lds[];
+  __shared__ int lmax;
+  const int T1 = t + 1;
+  const int G = blockDim.x / T1;
+  const int r = threadIdx.x / T1, k = threadIdx.x % T1;
+  const int f = blockIdx.x * G + r;
+  const bool active = r < G && f < nfd;
+  if (threadIdx.x == 0) lmax = 0;
+  __syncthreads();
+  int L = 0;
+  size_t off = 0;
+  Jac<Fp> D = jac_zero<Fp>();
+  if (active) {
+    L = (int)fd_len[f];
+    off = fd_off[f];
+    D = jac_load(ebuf + (off + k) * FD_WORDS);
+    atomicMax(&lmax, L);
+  }
+  __syncthreads();
+  uint32_t* mine = fd_lds + (size_t)threadIdx.x * FD_WORDS;
+  // forward differences at y0: level lv, D_k -= D_{k-1} for k >= lv
+  for (int lv = 1; lv <= t; lv++) {
+    if (active) jac_store(mine, D);
+    __syncthreads();
+    if (active && k >= lv) D = jac_add(D, jac_neg(jac_load(mine - FD_WORDS)));
+    __syncthreads();
+  }
+  // step s moves the table from y0 + s - 1 to y0 + s; D_0 = E(y0 + s); values s <= t are known
+  const int steps = lmax;
+  for (int s = 1; s < steps; s++) {
+    if (active) jac_store(mine, D);
+    __syncthreads();
+    if (active && k < t && s < L) D = jac_add(D, jac_load(mine + FD_WORDS));
+    __syncthreads();
+    if (active && k == 0 && s > t && s < L) jac_store(ebuf + (off + s) * FD_WORDS, D);
+  }
+}
+
+// step 4: ack a = list[k] compares E at epos[a] with g1 * val (comb table)
+__global__ void __launch_bounds__(256) k_bivar_fd_check(int n, const uint32_t* __restrict__ ebuf,
+                                                        const uint32_t* __restrict__ epos,
+                                                        const uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ fbtab,
+                                                        const uint32_t* __restrict__ list, uint8_t* __restrict__ verdict) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int a = (int)list[k];
+  const Jac<Fp> e = jac_load(ebuf + (size_t)epos[a] * FD_WORDS);
+  uint32_t ks[8];
+  for (int j = 0; j < 8; j++) ks[j] = vals[(size_t)a * 8 + j];
+  verdict[a] = jac_eq(e, fb_mul(fbtab, ks)) ? 1 : 0;
+}
+
 // Commitment::evaluate(x) = sum_j C_j x^j (threshold_crypto poly.rs) by Horner in G1 with the small
 // integer x -- PublicKeySet::public_key_share(i) = evaluate(i + 1), precomputed for every node by
 // NetworkInfo::new (src/network_info.rs:59-62).  commits holds ncommit commitments of t+1 points;
@@ -568,6 +684,26 @@ hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const u
   if (nack <= 0) return hipSuccess;
   hipLaunchKernelGGL(hb::k_bivar_check, grid_for(nack), dim3(256), 0, s, nack, t, (const uint32_t*)rows, row_idx, ys,
                      vals, (const uint32_t*)fbtab, order, verdict);
+  return hipGetLastError();
+}
+
+size_t fd_point_bytes() { return (size_t)hb::FD_WORDS * 4; }
+hipError_t bivar_fd(hipStream_t s, int nfd, int t, const void* rows, const uint32_t* fd_slot, const uint32_t* fd_y0,
+                    const uint32_t* fd_off, const uint32_t* fd_len, void* ebuf) {
+  if (nfd <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_bivar_fd_horner, grid_for(nfd * (t + 1)), dim3(256), 0, s, nfd, t, (const uint32_t*)rows,
+                     fd_slot, fd_y0, fd_off, (uint32_t*)ebuf);
+  const int G = 256 / (t + 1);
+  const size_t lds = (size_t)256 * hb::FD_WORDS * 4;
+  hipLaunchKernelGGL(hb::k_bivar_fd_run, dim3((unsigned)((nfd + G - 1) / G)), dim3(256), lds, s, nfd, t, fd_off, fd_len,
+                     (uint32_t*)ebuf);
+  return hipGetLastError();
+}
+hipError_t bivar_fd_check(hipStream_t s, int n, const void* ebuf, const uint32_t* epos, const uint32_t* vals,
+                          const void* fbtab, const uint32_t* list, uint8_t* verdict) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hb::k_bivar_fd_check, grid_for(n), dim3(256), 0, s, n, (const uint32_t*)ebuf, epos, vals,
+                     (const uint32_t*)fbtab, list, verdict);
   return hipGetLastError();
 }
 

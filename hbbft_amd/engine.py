@@ -343,7 +343,8 @@ class Engine:
         check(self._l.hbh_engine_set_pairing_impl(self._h, int(impl)))
 
     def set_ack_impl(self, impl):
-        """HBH_ACK_*: 0 = auto (default), 1 = lane quads, 2 = one lane per ack (commitment sets)."""
+        """HBH_ACK_*: 0 = auto (default), 1 = lane quads, 2 = one lane per ack (finite differences for
+        dense y runs), 3 = one lane per ack, Horner only (commitment sets)."""
         check(self._l.hbh_engine_set_ack_impl(self._h, int(impl)))
 
     # ------------------------------------------------------------ profiling

@@ -106,3 +106,15 @@ def bivar_ack(t, y, val_windows=32):
     cross-multiplied compare."""
     horner = _scale(_add(g1_mul_small(y), G1_MADD), t + 1)
     return _add(horner, _scale(G1_MADD, val_windows), (4, 2))
+
+
+def bivar_row_fd(t, y0, span, nacks, val_windows=32):
+    """The finite-difference Ack check of one row (k_bivar_fd_horner / _run / _check): Horner at the
+    t + 1 points y0 .. y0 + t, the t (t + 1) / 2 subtractions of the forward-difference table, t
+    additions per further y (span - t - 1 of them; the run kernel also replays the t known points,
+    which are not counted here), and per ack g1 * val from the comb table and the compare."""
+    horner = _add(*[_scale(_add(g1_mul_small(y), G1_MADD), t + 1) for y in range(y0, y0 + t + 1)])
+    table = _scale(G1_ADD, t * (t + 1) // 2)
+    steps = _scale(G1_ADD, t * max(0, span - t - 1))
+    acks = _scale(_add(_scale(G1_MADD, val_windows), (4, 2)), nacks)
+    return _add(horner, table, steps, acks)

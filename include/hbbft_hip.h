@@ -355,10 +355,15 @@ int hbh_engine_set_pairing_impl(hbh_engine* eng, int impl);
  * split each G1 operation, Jacobian rows -- latency), HBH_ACK_LANE (k_bivar_check: one lane per ack,
  * affine rows and mixed additions -- throughput), HBH_ACK_AUTO (default: LANE from HBH_ACK_LANE_MIN
  * acks per call; measured crossover ~50,000 acks, profiles/r03/ack_kernel_sweep.txt: 40,000 acks
- * quad 6.4 / lane 7.0 ms, 160,000 acks 18.9 / 13.1 ms, 10^6 acks 112 / 53 ms).  Same verdicts. */
+ * quad 6.4 / lane 7.0 ms, 160,000 acks 18.9 / 13.1 ms, 10^6 acks 112 / 53 ms).  Same verdicts.
+ * Round 5: on the LANE path (and AUTO's), the acks of a row whose y form a dense run (>= 2 (t + 1) acks
+ * over <= twice as many consecutive y: a node's drain, one Ack per sender per Part) are checked by
+ * finite differences -- t + 1 Horner points, then t G1 additions per further y;
+ * HBH_ACK_LANE_HORNER keeps every ack on the Horner kernel (A/B, parity tests). */
 #define HBH_ACK_AUTO 0
 #define HBH_ACK_QUAD 1
 #define HBH_ACK_LANE 2
+#define HBH_ACK_LANE_HORNER 3
 #define HBH_ACK_LANE_MIN 65536
 int hbh_engine_set_ack_impl(hbh_engine* eng, int impl);
 

@@ -14,7 +14,7 @@ import pytest
 
 from oracle import bls12_381 as C
 from oracle import cbls
-from hbbft_amd._lib import ACK_AUTO, ACK_LANE, ACK_QUAD, HbhError
+from hbbft_amd._lib import ACK_AUTO, ACK_LANE, ACK_LANE_HORNER, ACK_QUAD, HbhError
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a
 
 pytestmark = pytest.mark.gpu
@@ -90,6 +90,64 @@ def test_config3_network_acks(engine):
         lhs = cbls.bivar_evaluate(t, commits[int(pidx[a])], int(xs[a]), int(ys[a]))
         rhs = cbls.g1_mul(G1, int.from_bytes(bytes(vals[a]), "little"))
         assert (lhs == rhs) == bool(got[a]), a
+    cs.close()
+
+
+@pytest.mark.parametrize("t", [33, 5, 1])
+def test_ack_finite_differences_match_horner(engine, t):
+    """Round 5: the one-lane Ack path checks the acks of a row whose y form a dense run by finite
+    differences (hbl::bivar_fd: Horner at t + 1 points, the forward-difference table, t G1 additions
+    per further y).  Rows of every shape -- a node's full run y = 1..100, runs with gaps, a run not
+    starting at 1, duplicated y, a run of exactly 2 (t + 1) acks, a longer run, and sparse rows that
+    stay on Horner -- with 1/11 tampered values: FD verdicts == Horner-only == lane quads == the
+    construction, plus C-oracle samples (BivarCommitment::evaluate == g1 * val, sync_key_gen.rs:542)."""
+    from hbbft_amd import hoststage
+    rng = random.Random(700 + t)
+    T1 = t + 1
+    npos = T1 * (t + 2) // 2
+    nparts = 6
+    coefs = [[rng.randrange(R) for _ in range(npos)] for _ in range(nparts)]
+    flat = engine.g1_mul_gen([c for cs in coefs for c in cs])
+    commits = [flat[p * npos:(p + 1) * npos] for p in range(nparts)]
+    runs = [(0, 1, list(range(1, 101))),
+            (0, 2, [y for y in range(1, 101) if y % 5]),
+            (1, 1, list(range(50, 150))),
+            (1, 2, [y for y in range(1, 71) for _ in range(2)]),
+            (2, 1, sorted(rng.sample(range(1, 1000), 30))),
+            (3, 1, list(range(1, 2 * T1 + 1))),
+            (4, 7, list(range(1, 201))),
+            (5, 3, list(range(1, T1 + 2)))]
+    acks = [(p, x, y) for p, x, ys in runs for y in ys]
+    rng.shuffle(acks)
+    # vals: row(x) of part p is the polynomial in y with coefficients sum_i c(i, j) x^i
+    rowpoly = {}
+    for p, x, _ in runs:
+        ev = hoststage.fr_poly_eval([[coefs[p][cp(i, j)] for i in range(T1)] for j in range(T1)], [x])
+        rowpoly[(p, x)] = [ev[j][0] for j in range(T1)]
+    keys = sorted(rowpoly)
+    ys_all = sorted({y for _, _, y in acks})
+    table = dict(zip(keys, hoststage.fr_poly_eval([rowpoly[k] for k in keys], ys_all)))
+    yi = {y: k for k, y in enumerate(ys_all)}
+    vals = [table[(p, x)][yi[y]] for p, x, y in acks]
+    bad = set(range(3, len(acks), 11))
+    vals = [(v + 1) % R if a in bad else v for a, v in enumerate(vals)]
+    want = bytes(0 if a in bad else 1 for a in range(len(acks)))
+    args = ([a[0] for a in acks], [a[1] for a in acks], [a[2] for a in acks], vals)
+    cs = engine.commit_set(t)
+    cs.add(commits)
+    got = {}
+    try:
+        for impl in (ACK_LANE, ACK_LANE_HORNER, ACK_QUAD, ACK_LANE):
+            engine.set_ack_impl(impl)
+            got[impl] = cs.ack_check(*args)
+            assert got[impl] == want, impl
+    finally:
+        engine.set_ack_impl(ACK_AUTO)
+    for a in sorted(rng.sample(range(len(acks)), 6)) + sorted(bad)[:2]:
+        p, x, y = acks[a]
+        lhs = cbls.bivar_evaluate(t, commits[p], x, y)
+        rhs = cbls.g1_mul(G1, vals[a])
+        assert (lhs == rhs) == bool(want[a]), a
     cs.close()
 
 
