@@ -132,7 +132,8 @@ struct hbh_engine {
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
   // Ack checks of dense y runs by finite differences (hbl::bivar_fd); HBH_ACK_FD=0: Horner only (A/B)
   bool ack_fd = true;
-  DevBuf fd_e, fd_meta;
+  DevBuf fd_e, fd_meta, fb16;
+  bool fb16_ready = false;  // 16-bit comb of g1 (the FD ack check), built on first use
   size_t split_max = 0;  // HBH_SPLIT_MAX: most combines per call on the split check (0: the wave rule)
   // commitment sets created on this engine: hbh_engine_destroy frees their device memory and
   // detaches them, so a set destroyed after its engine never touches the freed engine
@@ -383,7 +384,7 @@ int hbh_engine_destroy(hbh_engine* e) {
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
                     &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval, &e->split_in,
-                    &e->split_out, &e->fd_e, &e->fd_meta})
+                    &e->split_out, &e->fd_e, &e->fd_meta, &e->fb16})
     b->release();
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   (void)hipEventDestroy(e->done);
@@ -573,6 +574,19 @@ int ensure_fbtab(hbh_engine* e, hipStream_t s) {
   HBH_CHECK(e->fbtab.ensure(hbl::fb_table_bytes()));
   HBH_CHECK(hbl::fb_table(s, e->fbtab.p));
   e->fbtab_ready = true;
+  return HBH_OK;
+}
+
+int ensure_fb16(hbh_engine* e, hipStream_t s) {
+  if (e->fb16_ready) return HBH_OK;
+  HBH_CHECK(e->fb16.ensure(hbl::fb16_table_bytes()));
+  DevBuf scratch;  // freed before return, also on failure
+  hipError_t err = scratch.ensure(hbl::fb16_scratch_bytes());
+  if (err == hipSuccess) err = hbl::fb16_table(s, e->fb16.p, scratch.p);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  scratch.release();
+  HBH_CHECK(err);
+  e->fb16_ready = true;
   return HBH_OK;
 }
 
@@ -1804,6 +1818,8 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
   const size_t nfd = fd.slot.size();
   uint32_t* d_fd = nullptr;
   if (nfd) {
+    rc = ensure_fb16(e, s);
+    if (rc) return rc;
     const size_t words = 4 * nfd + 2 * nack;
     HBH_CHECK(e->fd_meta.ensure(words * 4));
     HBH_CHECK(e->fd_e.ensure(fd.npts * hbl::fd_point_bytes()));
@@ -1820,7 +1836,7 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
     HBH_CHECK(hbl::bivar_fd(s, (int)nfd, t, cs->rows[1].p, d_fd, d_fd + nfd, d_fd + 2 * nfd, d_fd + 3 * nfd,
                             e->fd_e.p));
     HBH_CHECK(hbl::bivar_fd_check(s, (int)fd.fd_acks.size(), e->fd_e.p, d_fd + 4 * nfd, (const uint32_t*)e->in_c.p,
-                                  e->fbtab.p, d_fd + 4 * nfd + nack, (uint8_t*)e->out_v.p));
+                                  e->fb16.p, d_fd + 4 * nfd + nack, (uint8_t*)e->out_v.p));
     HBH_CHECK(hbl::bivar_check(s, (int)order.size(), t, cs->rows[1].p, d_ro, d_y, (const uint32_t*)e->in_c.p,
                                e->fbtab.p, (uint8_t*)e->out_v.p, d_ord));
   } else if (lane)

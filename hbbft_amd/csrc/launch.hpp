@@ -93,12 +93,17 @@ hipError_t bivar_check_quad(hipStream_t s, int nack, int t, const void* rows, co
 // Ack checks by finite differences over dense runs of y (k_curve.hip): FD row f evaluates the affine row
 // slot fd_slot[f] at y = fd_y0[f] .. fd_y0[f] + fd_len[f] - 1 (fd_len >= t + 1) into ebuf from point
 // fd_off[f] on (fd_point_bytes() each); bivar_fd_check then compares ack list[k]'s point epos[a] with
-// g1 * val.  t + 1 <= 256.
+// g1 * val from the 16-bit comb fb16 (fb16_table).  t + 1 <= 256.
 size_t fd_point_bytes();
+// 16-bit fixed-base comb of g1 for bivar_fd_check (16 windows x 65,536 affine points, fb16_table_bytes()),
+// built once through fb16_scratch_bytes() of scratch
+size_t fb16_table_bytes();
+size_t fb16_scratch_bytes();
+hipError_t fb16_table(hipStream_t s, void* tab, void* scratch);
 hipError_t bivar_fd(hipStream_t s, int nfd, int t, const void* rows, const uint32_t* fd_slot, const uint32_t* fd_y0,
                     const uint32_t* fd_off, const uint32_t* fd_len, void* ebuf);
 hipError_t bivar_fd_check(hipStream_t s, int n, const void* ebuf, const uint32_t* epos, const uint32_t* vals,
-                          const void* fbtab, const uint32_t* list, uint8_t* verdict);
+                          const void* fb16, const uint32_t* list, uint8_t* verdict);
 hipError_t bivar_check(hipStream_t s, int nack, int t, const void* rows, const uint32_t* row_idx, const uint32_t* ys,
                        const uint32_t* vals, const void* fbtab, uint8_t* verdict, const uint32_t* order = nullptr);
 // Fixed-base comb table of the G1 generator (32 windows x 256 affine points, fb_table_bytes()) and
