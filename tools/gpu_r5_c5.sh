@@ -17,3 +17,7 @@ cd /tmp
 mkdir -p $O/trace
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --workload dkg --steps 4 --no-cpu-baseline --no-node-round > $O/trace/run.log 2>&1 || { echo "trace failed"; tail -5 $O/trace/run.log; exit 1; }
 find $O/trace -name "*kernel_stats.csv" -exec head -8 {} \;
+mkdir -p $O/combine
+timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d $O/combine -o run -- python3 $R/tools/combine_trace.py --reps 20 > $O/combine/run.log 2>&1 || { echo "combine trace failed"; tail -5 $O/combine/run.log; exit 1; }
+tail -1 $O/combine/run.log
+python3 $R/tools/combine_trace.py --trace $O/combine > $O/combine/anatomy.txt; cat $O/combine/anatomy.txt | head -40
