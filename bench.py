@@ -887,7 +887,7 @@ def run_dkg(args, eng, world, rank, dev):
         else:
             ops = [workcount.bivar_ack(t, y) for y in range(1, n_nodes + 1)]
             op = (sum(o[0] for o in ops) / n_nodes, sum(o[1] for o in ops) / n_nodes)
-        kname = ("hb::k_bivar_fd_horner + hb::k_bivar_fd_run + hb::k_bivar_fd_check" if fd else
+        kname = ("hb::k_bivar_fd_seed + hb::k_bivar_fd_run + hb::k_bivar_fd_check" if fd else
                  "hb::k_bivar_check" if lane else "hbs::k_bivar_check_quad")
         waves = (1 if lane else 4) * nack / 64 / 1024
         main_k = roofline_entry(kname, dev_n, dev_ms, nack, op, "ack check", waves)

@@ -1592,10 +1592,12 @@ int set_rows(hbh_commit_set* cs, hipStream_t s, bool affine, size_t n, const uin
 
 // Finite-difference plan of an Ack drain (hbl::bivar_fd): a row slot whose acks form a dense run of y
 // -- at least 2 (t + 1) acks spanning at most twice as many consecutive y, as a node's drain has (one
-// Ack per sender per Part) -- is evaluated at every y of its span by t + 1 Horner points and t
-// additions per further y; its acks then compare against those points (epos).  Every other ack takes
-// the Horner kernel (other, in order of y).  FD rows are sorted by span length (the run kernel's
-// workgroups step their rows together).
+// Ack per sender per Part) -- is evaluated at every y of its span from the difference table at y0 (the
+// seed levels: (t+1)(t+2)/2 small products) and t additions per further y; its acks then compare
+// against those points (epos).  y0 = 0 when the run starts at y <= t + 1 (the seed's products are then
+// one per entry, worth the few extra steps), else the run's first y.  Every other ack takes the Horner
+// kernel (other, in order of y).  FD rows are sorted by span length (the run kernel's workgroups step
+// their rows together); a span is at least 2 (t + 1) points (the seed's two tables live in it).
 struct FdPlan {
   std::vector<uint32_t> slot, y0, off, len;  // per FD row
   std::vector<uint32_t> epos;                // per ack (FD acks only)
@@ -1616,8 +1618,10 @@ void plan_fd(size_t n, const std::vector<uint32_t>& slot, const uint32_t* ys, in
   std::vector<uint32_t> cand;
   for (uint32_t s = 0; s < nslot; s++) {
     if (!cnt[s] || T1 > 128) continue;
+    if (ymin[s] <= T1) ymin[s] = 0;  // seed at y0 = 0
     const uint64_t span = (uint64_t)ymax[s] - ymin[s] + 1;
-    if (cnt[s] >= 2 * T1 && span <= 2 * (uint64_t)cnt[s] && span > T1 && span < ((uint64_t)1 << 20)) cand.push_back(s);
+    if (cnt[s] >= 2 * T1 && span >= 2 * T1 && span <= 2 * (uint64_t)cnt[s] && span < ((uint64_t)1 << 20))
+      cand.push_back(s);
   }
   std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) {
     const uint32_t la = ymax[a] - ymin[a], lb = ymax[b] - ymin[b];
@@ -1629,7 +1633,7 @@ void plan_fd(size_t n, const std::vector<uint32_t>& slot, const uint32_t* ys, in
     P.slot.push_back(s);
     P.y0.push_back(ymin[s]);
     P.off.push_back((uint32_t)P.npts);
-    P.len.push_back(ymax[s] - ymin[s] + 1);
+    P.len.push_back(ymax[s] - ymin[s] + 1);  // >= 2 (t + 1)
     P.npts += ymax[s] - ymin[s] + 1;
   }
   P.epos.assign(n, 0);

@@ -492,13 +492,18 @@ __global__ void __launch_bounds__(256) k_bivar_check(int nack, int t, const uint
 // The acks of one row R = row(x) (one Part, one checking node x) evaluate the same degree-t polynomial
 // E(y) = sum_j R_j y^j at the senders' y = 1..N.  For a dense run of y (a row with many acks, as every
 // node's Ack drain has: one Ack per sender per Part) E is evaluated at y0 .. y0 + L - 1 as
-//   1. Horner at the first t + 1 points (k_bivar_fd_horner, one lane per point),
-//   2. the forward-difference table D_k = Delta^k E(y0) of those points (t levels of subtractions),
-//   3. D_k += D_{k+1} (k < t) per step of y: every further E(y) costs t independent G1 additions
-//      instead of a Horner of t steps by a small scalar (k_bivar_fd_run: one lane per (row, k)),
+//   1. the forward-difference table D_k = Delta^k E(y0), k <= t, straight from the row: with the
+//      Horner tails F_m(y) = R_m + y F_{m+1}(y) (F_t = R_t, F_0 = E) the product rule of differences
+//      gives  Delta^k F_m(y0) = [k = 0] R_m + (y0 + k) Delta^k F_{m+1}(y0) + k Delta^{k-1} F_{m+1}(y0),
+//      one level per m (k_bivar_fd_seed, one launch per level, lane (k, row) k-major so a wave's lanes
+//      share the small multipliers); for y0 = 0 a level entry is one product k (D_k + D_{k-1}), so the
+//      table costs (t+1)(t+2)/2 small products per row where Horner at t+1 points cost (t+1) t,
+//   2. D_k += D_{k+1} (k < t) per step of y: every further E(y) costs t independent G1 additions
+//      (k_bivar_fd_run: one lane per (row, k)),
 // and each ack compares its E(y) with g1 * val (k_bivar_fd_check).  Exact group arithmetic throughout:
 // the verdicts are the Horner kernel's bit for bit (tests/test_gpu_commit_set.py compares them).
-// E values are stored as Jacobian points (FD_WORDS words each).
+// E values are stored as Jacobian points (FD_WORDS words each); a row's region of L >= 2 (t + 1) points
+// holds the seed levels' two tables (level m in slots (m & 1) (t + 1) + k) before the run fills it.
 constexpr int FD_WORDS = 3 * NL;
 
 __device__ __forceinline__ void jac_store(uint32_t* __restrict__ w, const Jac<Fp>& p) {
@@ -520,33 +525,39 @@ __device__ __forceinline__ Jac<Fp> jac_load(const uint32_t* __restrict__ w) {
   return p;
 }
 
-// E(y) = sum_j R_j y^j by Horner with the small y over an affine row
-__device__ __forceinline__ Jac<Fp> row_horner(const uint32_t* __restrict__ R, int t, uint32_t y) {
-  Jac<Fp> acc = jac_zero<Fp>();
-  for (int j = t; j >= 0; j--) {
-    acc = jac_mul_small(acc, y);
+// step 1, level m: lane g = k * nfd + f (k <= t - m) writes Delta^k F_m(y0[f]) of FD row f; level t
+// is F_t = R_t itself.
+__global__ void __launch_bounds__(256) k_bivar_fd_seed(int nfd, int t, int m, const uint32_t* __restrict__ rows,
+                                                       const uint32_t* __restrict__ fd_slot,
+                                                       const uint32_t* __restrict__ fd_y0,
+                                                       const uint32_t* __restrict__ fd_off, uint32_t* __restrict__ ebuf) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int deg = t - m;  // degree of F_m
+  if (g >= nfd * (deg + 1)) return;
+  const int k = g / nfd, f = g % nfd;
+  const size_t T1 = (size_t)t + 1;
+  uint32_t* E = ebuf + (size_t)fd_off[f] * FD_WORDS;
+  const uint32_t* in = E + ((m + 1) & 1) * T1 * FD_WORDS;
+  Jac<Fp> d = jac_zero<Fp>();
+  if (m < t) {
+    const Jac<Fp> a = k < deg ? jac_load(in + (size_t)k * FD_WORDS) : jac_zero<Fp>();
+    const Jac<Fp> b = k > 0 ? jac_load(in + (size_t)(k - 1) * FD_WORDS) : jac_zero<Fp>();
+    const uint32_t y0 = fd_y0[f];
+    if (y0 == 0)
+      d = jac_mul_small(jac_add(a, b), (uint32_t)k);
+    else
+      d = jac_add(jac_mul_small(a, y0 + (uint32_t)k), jac_mul_small(b, (uint32_t)k));
+  }
+  if (k == 0) {
     Fp rx, ry;
     bool inf;
-    load_g1(R + (size_t)j * G1_WORDS, rx, ry, inf);
-    if (!inf) acc = jac_add_affine(acc, rx, ry);
+    load_g1(rows + ((size_t)fd_slot[f] * T1 + m) * G1_WORDS, rx, ry, inf);
+    if (!inf) d = jac_add_affine(d, rx, ry);
   }
-  return acc;
+  jac_store(E + ((m & 1) * T1 + k) * FD_WORDS, d);
 }
 
-// step 1: lane g = i * nfd + f evaluates FD row f at y0[f] + i (i <= t); i-major, so the lanes of a
-// wave share i (and y, for rows of one y0: the small-scalar chains do not diverge)
-__global__ void __launch_bounds__(256) k_bivar_fd_horner(int nfd, int t, const uint32_t* __restrict__ rows,
-                                                         const uint32_t* __restrict__ fd_slot,
-                                                         const uint32_t* __restrict__ fd_y0,
-                                                         const uint32_t* __restrict__ fd_off, uint32_t* __restrict__ ebuf) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= nfd * (t + 1)) return;
-  const int i = g / nfd, f = g % nfd;
-  const uint32_t* R = rows + (size_t)fd_slot[f] * (t + 1) * G1_WORDS;
-  jac_store(ebuf + ((size_t)fd_off[f] + i) * FD_WORDS, row_horner(R, t, fd_y0[f] + (uint32_t)i));
-}
-
-// steps 2-3: one workgroup per G = blockDim / (t + 1) FD rows, lane (r, k) holds D_k of row r; the
+// step 2: one workgroup per G = blockDim / (t + 1) FD rows, lane (r, k) holds D_k of row r; the
 // neighbour's D crosses lanes through LDS (blockDim x FD_WORDS words).  Rows are sorted by length, so
 // a workgroup's rows step together; a row stops at its own length.
 __global__ void __launch_bounds__(256) k_bivar_fd_run(int nfd, int t, const uint32_t* __restrict__ fd_off,
@@ -571,21 +582,14 @@ __global__ void __launch_bounds__(256) k_bivar_fd_run(int nfd, int t, const uint
   }
   __syncthreads();
   uint32_t* mine = fd_lds + (size_t)threadIdx.x * FD_WORDS;
-  // forward differences at y0: level lv, D_k -= D_{k-1} for k >= lv
-  for (int lv = 1; lv <= t; lv++) {
-    if (active) jac_store(mine, D);
-    __syncthreads();
-    if (active && k >= lv) D = jac_add(D, jac_neg(jac_load(mine - FD_WORDS)));
-    __syncthreads();
-  }
-  // step s moves the table from y0 + s - 1 to y0 + s; D_0 = E(y0 + s); values s <= t are known
+  // step s moves the table from y0 + s - 1 to y0 + s; D_0 = E(y0 + s) (E(y0) = D_0 is in slot 0)
   const int steps = lmax;
   for (int s = 1; s < steps; s++) {
     if (active) jac_store(mine, D);
     __syncthreads();
     if (active && k < t && s < L) D = jac_add(D, jac_load(mine + FD_WORDS));
     __syncthreads();
-    if (active && k == 0 && s > t && s < L) jac_store(ebuf + (off + s) * FD_WORDS, D);
+    if (active && k == 0 && s < L) jac_store(ebuf + (off + s) * FD_WORDS, D);
   }
 }
 
@@ -762,8 +766,9 @@ size_t fd_point_bytes() { return (size_t)hb::FD_WORDS * 4; }
 hipError_t bivar_fd(hipStream_t s, int nfd, int t, const void* rows, const uint32_t* fd_slot, const uint32_t* fd_y0,
                     const uint32_t* fd_off, const uint32_t* fd_len, void* ebuf) {
   if (nfd <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hb::k_bivar_fd_horner, grid_for(nfd * (t + 1)), dim3(256), 0, s, nfd, t, (const uint32_t*)rows,
-                     fd_slot, fd_y0, fd_off, (uint32_t*)ebuf);
+  for (int m = t; m >= 0; m--)
+    hipLaunchKernelGGL(hb::k_bivar_fd_seed, grid_for(nfd * (t - m + 1)), dim3(256), 0, s, nfd, t, m,
+                       (const uint32_t*)rows, fd_slot, fd_y0, fd_off, (uint32_t*)ebuf);
   const int G = 256 / (t + 1);
   const size_t lds = (size_t)256 * hb::FD_WORDS * 4;
   hipLaunchKernelGGL(hb::k_bivar_fd_run, dim3((unsigned)((nfd + G - 1) / G)), dim3(256), lds, s, nfd, t, fd_off, fd_len,

@@ -108,13 +108,20 @@ def bivar_ack(t, y, val_windows=32):
     return _add(horner, _scale(G1_MADD, val_windows), (4, 2))
 
 
-def bivar_row_fd(t, y0, span, nacks, val_windows=32):
-    """The finite-difference Ack check of one row (k_bivar_fd_horner / _run / _check): Horner at the
-    t + 1 points y0 .. y0 + t, the t (t + 1) / 2 subtractions of the forward-difference table, t
-    additions per further y (span - t - 1 of them; the run kernel also replays the t known points,
-    which are not counted here), and per ack g1 * val from the comb table and the compare."""
-    horner = _add(*[_scale(_add(g1_mul_small(y), G1_MADD), t + 1) for y in range(y0, y0 + t + 1)])
-    table = _scale(G1_ADD, t * (t + 1) // 2)
-    steps = _scale(G1_ADD, t * max(0, span - t - 1))
+def bivar_row_fd(t, ymin, ymax, nacks, val_windows=16):
+    """The finite-difference Ack check of one row (k_bivar_fd_seed / _run / _check): the difference
+    table at y0 (0 when ymin <= t + 1, as the engine's plan_fd seeds) by the seed levels -- per level
+    m < t and k = 1 .. t - m one product k (D_k + D_{k-1}) for y0 = 0, else (y0 + k) D_k + k D_{k-1},
+    and per level one mixed addition of R_m --, t additions per further y (ymax - y0 steps), and per
+    ack g1 * val from the 16-bit comb (one mixed addition per nonzero 16-bit window) and the compare."""
+    y0 = 0 if ymin <= t + 1 else ymin
+    parts = [_scale(G1_MADD, t + 1)]
+    for m in range(t - 1, -1, -1):
+        for k in range(1, t - m + 1):
+            if y0 == 0:
+                parts.append(_add(G1_ADD, g1_mul_small(k)))
+            else:
+                parts.append(_add(G1_ADD, g1_mul_small(y0 + k), g1_mul_small(k)))
+    steps = _scale(G1_ADD, t * (ymax - y0))
     acks = _scale(_add(_scale(G1_MADD, val_windows), (4, 2)), nacks)
-    return _add(horner, table, steps, acks)
+    return _add(*parts, steps, acks)
