@@ -9,10 +9,14 @@ faults (too far in the future :250-251, a second coin share of one sender for on
 :100-105), the decision rule (:411-432) -- and runs every coin share check through the
 ``BatchVerifier`` (hbbft_amd.protocol), i.e. batched on the GPU.
 
-Out of scope: the Synchronized Binary Value broadcast and the Conf round (BVal / Aux /
-Conf / Term vote counting).  Their outcome -- the aux values an epoch's SBV broadcast outputs, and the completion of its
-Conf round -- is handed in by the driver (``sbv_output``, ``conf_round_complete``) at the points where
-the reference's handle_sbvb_step (:301-324) and try_finish_conf_round (:469-480) act on it.
+Two forms.  ``BinaryAgreementCoin`` is the coin path alone, driven by the HoneyBadger epoch flows
+(honey_badger.py): the outcome of an epoch's SBV broadcast and Conf round (``sbv_output``,
+``conf_round_complete``) is handed in by the driver at the points where handle_sbvb_step (:301-324)
+and try_finish_conf_round (:469-480) act on it.  ``BinaryAgreement`` (round 5) is the whole
+instance -- SbvBroadcast (sbv_broadcast.rs: BVal / Aux counting, bin_values), the Conf round, Term
+messages with expedited termination, the coin schedule and the future-epoch queue of every message
+kind -- for networks of instances (tests/test_binary_agreement_net_host.py, test_gpu_ba_network.py:
+the reference's tests/binary_agreement.rs and the reordering attack of binary_agreement_mitm.rs).
 """
 import struct
 

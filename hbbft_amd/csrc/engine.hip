@@ -126,10 +126,11 @@ struct hbh_engine {
   // (sign bench: 23.3 instead of 21.1 ms per 65,536-check step)
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
-  DevBuf fval, split_in, split_out;
+  DevBuf fval, split_in, split_out, tree_cnt;
   uint8_t* h_stage = nullptr;  // pinned host staging of the split check (one upload, one download)
   size_t h_stage_cap = 0;
   bool split_check = true;  // HBH_SPLIT_CHECK=0 in the environment: interpolate, then verify (A/B)
+  bool split_tree = true;   // HBH_SPLIT_TREE=0: a separate product + FE launch (wave_prod_fe) (A/B)
   // Ack checks of dense y runs by finite differences (hbl::bivar_fd); HBH_ACK_FD=0: Horner only (A/B)
   bool ack_fd = true;
   DevBuf fd_e, fd_meta, fb16;
@@ -347,6 +348,7 @@ int hbh_engine_create(int device, hbh_engine** out) {
   hbh_engine* e = new hbh_engine();
   e->device = device;
   if (const char* v = std::getenv("HBH_SPLIT_CHECK")) e->split_check = std::atoi(v) != 0;
+  if (const char* v = std::getenv("HBH_SPLIT_TREE")) e->split_tree = std::atoi(v) != 0;
   if (const char* v = std::getenv("HBH_ACK_FD")) e->ack_fd = std::atoi(v) != 0;
   if (const char* v = std::getenv("HBH_SPLIT_MAX")) e->split_max = (size_t)std::max(0, std::atoi(v));
   hipError_t err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
@@ -384,7 +386,7 @@ int hbh_engine_destroy(hbh_engine* e) {
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
                     &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval, &e->split_in,
-                    &e->split_out, &e->fd_e, &e->fd_meta, &e->fb16})
+                    &e->split_out, &e->tree_cnt, &e->fd_e, &e->fd_meta, &e->fb16})
     b->release();
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   (void)hipEventDestroy(e->done);
@@ -900,8 +902,10 @@ int run_interp(hbh_engine* e, size_t ncomb, int t, const uint32_t* idx, const ui
 //   prod_k e(lambda_k g1, sigma_k) * e(-mpk, H) == 1,
 // which needs no sigma: its m + 1 Miller loops (two pairs per wave, k_wave's Miller-only mode) run on a
 // second stream WHILE the engine stream interpolates sigma (one pair per wave, homogeneous walk: mode
-// W1J of tools/gen_wave_prog.py), and one wave per combine multiplies the
-// partial values and runs the single final exponentiation (wave_prod_fe).  The verdict is the same
+// W1J of tools/gen_wave_prog.py); in the same launch the partial values are multiplied up a binary tree
+// (the later of two sibling waves multiplies: log2(m + 1) products on the critical path instead of m)
+// and the wave holding a combine's product runs the single final exponentiation (wave_miller_tree;
+// HBH_SPLIT_TREE=0: a second launch multiplies the m + 1 values in order, wave_prod_fe).  The verdict is the same
 // boolean for every input (an exact identity, no randomisation); lambda_k g1 comes from the device comb
 // table summed in a 5-level tree on lane quads (k_g1_gen_quad) on the side stream, left in Jacobian
 // form: the Miller kernel scales each line by Z^3 instead of inverting Z (WAVE_JAC_P).  A repeated index gives zero
@@ -996,10 +1000,15 @@ int combine_verify_split(hbh_engine* e, size_t ncomb, size_t m, const std::vecto
     hbl::PairSideDesc sd0 = {din + o_p0, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i0), nq};
     hbl::PairSideDesc sd1 = {din + o_p1, din + o_q, nullptr, nullptr, (const uint32_t*)(din + o_i1), nq};
     hipEvent_t tp = e->timer.begin(s2, HBH_STAGE_PAIRING, e->profiling);
-    HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1,
-                               hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P | (pairs == 1 ? hbl::WAVE_ONE_SIDE : 0),
-                               nullptr, (uint32_t*)e->fval.p));
-    HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, dout + o_v));
+    const int wflags = hbl::WAVE_MILLER_ONLY | hbl::WAVE_JAC_P | (pairs == 1 ? hbl::WAVE_ONE_SIDE : 0);
+    if (e->split_tree) {  // product up a tree and the final exponentiation inside the Miller launch
+      HBH_CHECK(e->tree_cnt.ensure(hbl::wave_tree_counter_bytes((int)ncomb, (int)nw)));
+      HBH_CHECK(hbl::wave_miller_tree(s2, (int)ncomb, (int)nw, sd0, sd1, wflags, (uint32_t*)e->fval.p,
+                                      (uint32_t*)e->tree_cnt.p, dout + o_v));
+    } else {
+      HBH_CHECK(hbl::wave_verify(s2, (int)nchk, sd0, sd1, wflags, nullptr, (uint32_t*)e->fval.p));
+      HBH_CHECK(hbl::wave_prod_fe(s2, (int)ncomb, (int)nw, (const uint32_t*)e->fval.p, dout + o_v));
+    }
     e->timer.end(s2, tp);
     // engine stream, concurrently: the interpolation (lane-quad latency form, host digits)
     hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);

@@ -44,7 +44,10 @@ struct WaveArgs {
   uint32_t* value_out;  // 144 canonical words per check (may be null)
   const uint32_t* fin;  // product mode: nf Miller values (144 words, w-basis) per check; null otherwise
   int nf;
+  uint32_t* tree_cnt;   // tree mode (wave_miller_tree): arrival counters, TREE_LEVELS x tree_nw per group
+  int tree_nw;          // checks per group (0: no tree)
 };
+constexpr int TREE_LEVELS = 16;
 
 // ---------------------------------------------------------------- LDS slots
 HP_D Fp ld_own(const uint32_t* sm, int slot, int h) {
@@ -146,6 +149,55 @@ HP_D Fp wv_mul(const Fp (&x)[K], const Fp (&y)[K]) {
   return r;
 }
 
+// x * y in Fp (one lane, sfp.hpp fp_mul's product scanning) with each column in WV_NACC chains: the
+// same column sums, so the same output limbs as fp_mul, with a quarter of its dependent-MAD chain --
+// the lane-pair squares (h_sqr) of the CYC runs and square stages, where nothing else hides it
+HP_D Fp wv_fpmul(const Fp& x, const Fp& y) {
+  int32_t m[NL];
+  int64_t carry = 0;
+  Fp r;
+#pragma unroll
+  for (int k = 0; k < 2 * NL - 1; k++) {
+    int64_t acc[WV_NACC];
+#pragma unroll
+    for (int c = 0; c < WV_NACC; c++) acc[c] = 0;
+    int q = 0;
+    const int lo = k < NL ? 0 : k - NL + 1, hi = k < NL ? k : NL - 1;
+#pragma unroll
+    for (int i = lo; i <= hi; i++) acc[q++ % WV_NACC] += (int64_t)x.l[i] * y.l[k - i];
+#pragma unroll
+    for (int i = lo; i <= hi; i++)
+      if (i < k) acc[q++ % WV_NACC] += (int64_t)m[i] * (int32_t)P_L[k - i];
+    int64_t col = carry;
+#pragma unroll
+    for (int c = 0; c < WV_NACC; c++) {
+      if (WV_NACC > 1) asm("" : "+v"(acc[c]));
+      col += acc[c];
+    }
+    if (k < NL) {
+      m[k] = mont_digit(col);
+      col += (int64_t)m[k] * (int32_t)P_L[0];
+    } else {
+      r.l[k - NL] = (int32_t)col & MASK28;
+    }
+    carry = col >> 28;
+  }
+  r.l[NL - 1] = (int32_t)carry;
+  return r;
+}
+// pfp.hpp h_sqr with wv_fpmul
+HP_D Fp wv_sqr(const Fp& a) {
+  const bool ev = lp_even();
+  const Fp pa = dpp_fp<DPP_SWAP>(a);
+  Fp x, y;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    x.l[i] = pa.l[i] + (ev ? a.l[i] : pa.l[i]);
+    y.l[i] = a.l[i] - (ev ? pa.l[i] : 0);
+  }
+  return wv_fpmul(x, y);
+}
+
 template <int K>
 HP_D Fp product(const uint32_t* sm, int h, const uint64_t* d, uint32_t fl) {
   const bool xs = fl & 0x100, ys = fl & 0x200, sg = fl & 0xC00;
@@ -166,7 +218,7 @@ HP_D Fp product_sq(const uint32_t* sm, int h, uint64_t w, uint32_t fl) {
   const bool xs = fl & 0x100, sg = fl & 0xC00;
   const Fp x = operand(sm, h, (int)(w & 0xFF), (int)((w >> 8) & 0xFF), hi & 3, (hi >> 4) & 1, (hi >> 5) & 1, xs, sg,
                        xs || sg);
-  return h_sqr(x);
+  return wv_sqr(x);
 }
 
 // dst = sum c V + xi sum c' V' (8 x u16 descriptor: dst | gate << 8 | defone << 10, then terms
@@ -268,7 +320,7 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
   for (int it = 0; it < count; it++) {
     const Fp A = shfl_fp(v, base), B = shfl_fp(v, base + 4);
     const Fp x = j == 2 ? fp_add(A, B) : v;
-    const Fp sq = h_sqr(x);
+    const Fp sq = wv_sqr(x);
     const Fp sA = shfl_fp(sq, base), sB = shfl_fp(sq, base + 4), sAB = shfl_fp(sq, base + 8);
     const Fp L = shfl_fp(v, partner);
     // role 0 / 1: pair 0 -> X (r0 / r2), pair 1 -> Y (r3 / r5); role 2: pair 0 -> Z (r1), pair 1 -> X (r4)
@@ -517,12 +569,42 @@ __global__ void __launch_bounds__(64) k_wave(WaveArgs a) {
     if (!(a.flags & 16)) tl1 = wave_side<1>(a, sm, i, h, pair, act1, bad1);
     const bool bad = bad0 || bad1;
     if (bad) {  // index out of range: reject, never read past a table (uniform per workgroup)
-      if (lane == 0 && a.verdict) a.verdict[i] = 0;
+      if (lane == 0 && a.verdict && !a.tree_nw) a.verdict[i] = 0;  // tree mode: the group's stays 0
       return;
     }
     __syncthreads();
     const int mv = (a.flags & 16) ? 5 : (a.flags & 8) ? 4 : (a.s[0].lines ? 2 : 0) + (a.s[1].lines ? 1 : 0);
     run_stages(sm, hbw::WP_MILLER_OFF[mv], hbw::WP_MILLER_N[mv], h, pair, act0, act1, tl0, tl1);
+    if (a.tree_nw) {
+      // tree mode: node `node` of level L holds the product of checks [node 2^L, (node + 1) 2^L) of the
+      // group, published at the slot of its first check.  Of two siblings the later arrival (counter
+      // old value 1) multiplies and climbs; the earlier one leaves -- no wave ever waits on another.
+      const int nw = a.tree_nw, g = i / nw;
+      uint32_t* vals = a.value_out + (size_t)g * nw * 144;
+      int node = i - g * nw;
+      for (int L = 0; (1 << L) < nw; L++, node >>= 1) {
+        const int sib = node ^ 1;
+        if ((sib << L) >= nw) continue;  // no sibling at this level: the value climbs as it is
+        if (pair < 6) fp_to_words(ld_own(sm, hbw::WP_F + pair, h), vals + (size_t)(node << L) * 144 + 24 * pair + 12 * h);
+        __threadfence();  // release: the value is visible device-wide (every XCD) before the count
+        __syncthreads();
+        int old = 0;
+        if (lane == 0) old = (int)atomicAdd(a.tree_cnt + ((size_t)g * TREE_LEVELS + L) * nw + (node >> 1), 1u);
+        old = __shfl(old, 0);
+        if (old == 0) return;  // the sibling arrives later and carries on
+        __threadfence();       // acquire: the sibling's published value
+        wave_load12(sm, h, pair, hbw::WP_SIDE0, vals + (size_t)(sib << L) * 144);
+        __syncthreads();
+        run_stages(sm, hbw::WP_MULF_OFF, hbw::WP_MULF_N, h, pair, true, true, nullptr, nullptr);
+      }
+      __syncthreads();
+      run_stages(sm, hbw::WP_FE_OFF, hbw::WP_FE_N, h, pair, true, true, nullptr, nullptr);
+      bool ok = true;
+      if (pair < 6) ok = fp_is_zero(fp_sub(ld_own(sm, hbw::WP_E + pair, h), pair == 0 ? h_one() : h_zero()));
+      const bool all = __all(ok);
+      if (lane == 0 && a.verdict) a.verdict[g] = all ? 1 : 0;
+      return;
+    }
     if (a.flags & 4) {  // Miller only: f (w-basis) out, no final exponentiation
       if (pair < 6 && a.value_out)
         fp_to_words(ld_own(sm, hbw::WP_F + pair, h), a.value_out + (size_t)i * 144 + 24 * pair + 12 * h);
@@ -571,7 +653,39 @@ hipError_t wave_verify(hipStream_t s, int n, const PairSideDesc& d1, const PairS
   a.value_out = value_out;
   a.fin = nullptr;
   a.nf = 0;
+  a.tree_cnt = nullptr;
+  a.tree_nw = 0;
   hipLaunchKernelGGL(hbs::k_wave, dim3((unsigned)n), dim3(64), wave_lds_bytes(), s, a);
+  return hipGetLastError();
+}
+
+size_t wave_tree_counter_bytes(int ngroup, int nw) { return (size_t)ngroup * hbs::TREE_LEVELS * nw * 4; }
+hipError_t wave_miller_tree(hipStream_t s, int ngroup, int nw, const PairSideDesc& d1, const PairSideDesc& d2,
+                            int flags, uint32_t* value_out, uint32_t* counters, uint8_t* verdict) {
+  if (ngroup <= 0) return hipSuccess;
+  if (nw <= 0 || nw >= (1 << (hbs::TREE_LEVELS - 1)) || !value_out || !counters || !(flags & WAVE_MILLER_ONLY))
+    return hipErrorInvalidValue;
+  // a group whose tree never completes (a check index out of range) keeps verdict 0
+  hipError_t z = hipMemsetAsync(counters, 0, wave_tree_counter_bytes(ngroup, nw), s);
+  if (z == hipSuccess && verdict) z = hipMemsetAsync(verdict, 0, (size_t)ngroup, s);
+  if (z != hipSuccess) return z;
+  hbs::WaveArgs a = {};
+  a.n = ngroup * nw;
+  const PairSideDesc* d[2] = {&d1, &d2};
+  for (int k = 0; k < 2; k++) {
+    a.s[k].p = (const uint32_t*)d[k]->p;
+    a.s[k].q = (const uint32_t*)d[k]->q;
+    a.s[k].lines = (const int4*)d[k]->lines;
+    a.s[k].qinf = d[k]->qinf;
+    a.s[k].idx = d[k]->idx;
+    a.s[k].nq = (uint32_t)d[k]->nq;
+  }
+  a.flags = flags;
+  a.verdict = verdict;
+  a.value_out = value_out;
+  a.tree_cnt = counters;
+  a.tree_nw = nw;
+  hipLaunchKernelGGL(hbs::k_wave, dim3((unsigned)a.n), dim3(64), wave_lds_bytes(), s, a);
   return hipGetLastError();
 }
 

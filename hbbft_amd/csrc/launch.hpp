@@ -63,6 +63,15 @@ constexpr int WAVE_JAC_P = 8;
 // the homogeneous-walk Miller program (two stages per step instead of three)
 constexpr int WAVE_ONE_SIDE = 16;
 hipError_t wave_prod_fe(hipStream_t s, int n, int nf, const uint32_t* fin, uint8_t* verdict);
+// wave_verify's Miller-only mode with the product and the final exponentiation in the same launch:
+// the n = ngroup * nw checks form ngroup groups of nw consecutive checks; within a group the Miller
+// values are multiplied up a binary tree (the later-arriving wave of each sibling pair multiplies,
+// the other leaves), and the wave holding the group's product runs the final exponentiation:
+// verdict[g] = (FE(prod_k f_{g nw + k}) == 1).  value_out (n x 144 words) holds the tree's values;
+// counters: wave_tree_counter_bytes(ngroup, nw) bytes, zeroed by the launcher.
+size_t wave_tree_counter_bytes(int ngroup, int nw);
+hipError_t wave_miller_tree(hipStream_t s, int ngroup, int nw, const PairSideDesc& s1, const PairSideDesc& s2,
+                            int flags, uint32_t* value_out, uint32_t* counters, uint8_t* verdict);
 
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).

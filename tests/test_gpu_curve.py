@@ -153,8 +153,26 @@ def unsplit_engine():
     e.close()
 
 
+@pytest.fixture(scope="module")
+def notree_engine():
+    """An engine created with HBH_SPLIT_TREE=0: the split check multiplies the m + 1 Miller values in
+    order in a second launch (wave_prod_fe) instead of up a tree inside the Miller launch."""
+    from hbbft_amd.engine import Engine
+    old = os.environ.get("HBH_SPLIT_TREE")
+    os.environ["HBH_SPLIT_TREE"] = "0"
+    try:
+        e = Engine(0)
+    finally:
+        if old is None:
+            del os.environ["HBH_SPLIT_TREE"]
+        else:
+            os.environ["HBH_SPLIT_TREE"] = old
+    yield e
+    e.close()
+
+
 @pytest.mark.parametrize("t", [0, 1, 21, 70])
-def test_combine_verify_split_matches_unsplit(engine, unsplit_engine, t):
+def test_combine_verify_split_matches_unsplit(engine, unsplit_engine, notree_engine, t):
     """Calls of at most 540 + 24 t one-pair Miller waves (ncomb x (t + 2)) take the split master check
     (partial Miller loops of (lambda_k g1, sigma_k) and (-mpk, H) beside the interpolation, one final
     exponentiation per combine); larger calls, and an engine created with HBH_SPLIT_CHECK=0, the
@@ -185,6 +203,7 @@ def test_combine_verify_split_matches_unsplit(engine, unsplit_engine, t):
         hashes.append(h)
     out9, st9, v9 = unsplit_engine.combine_verify_g2(t, idx, pts, mpk, hashes)
     assert engine.combine_verify_g2(t, idx, pts, mpk, hashes) == (out9, st9, v9)
+    assert notree_engine.combine_verify_g2(t, idx, pts, mpk, hashes) == (out9, st9, v9)
     out8, st8, v8 = engine.combine_verify_g2(t, idx[:8], pts[:8], mpk, hashes[:8])
     out1, st1, v1 = engine.combine_verify_g2(t, idx[:1], pts[:1], mpk, hashes[:1])
     assert (out8, st8, v8) == (out9[:8], st9[:8], v9[:8])
