@@ -452,9 +452,10 @@ def main():
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
-    ap.add_argument("--prefetch-early", action="store_true",
-                    help="epoch workload: start the next epoch's coin prefetch with the epoch, beside the decryption prep")
-    ap.add_argument("--preverify-at", choices=["first_drain", "start"], default="first_drain",
+    ap.add_argument("--prefetch-after-prep", action="store_true",
+                    help="epoch workload: start the next epoch's coin prefetch once this epoch's decryption prep "
+                         "is done (round 4's order) instead of with the epoch (round 5 default, c16)")
+    ap.add_argument("--preverify-at", choices=["first_drain", "start"], default="start",
                     help="epoch workload: when the decryption-share pre-verification starts")
     ap.add_argument("--window", type=int, default=6144,
                     help="epoch workload: messages per verifier drain (6,144: 5 engine calls per epoch, 18.3-21.6 "
@@ -1078,18 +1079,19 @@ def run_epoch_bench(args, eng, world, rank, dev):
 
     def epoch_with_prefetch(k, tr, pf):
         # the next epoch's coin prefetch starts once this epoch's decryption prep has the host threads
-        # to itself (after_prep), unless --prefetch-early
+        # to itself (after_prep) with --prefetch-after-prep; by default with the epoch (round 5: the prep
+        # takes well under a millisecond, and the early prefetch measured 25.6-27.0 vs 22.4-23.9 epochs/s, c16)
         box, ev = [], threading.Event()
 
         def start_next():
             box.append(prefetch(k + 1))
             ev.set()
 
-        if args.prefetch_early:
+        if not args.prefetch_after_prep:
             start_next()
         r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf,
                       preverify=not args.no_preverify, preverify_at=args.preverify_at,
-                      after_prep=None if args.prefetch_early else start_next)
+                      after_prep=start_next if args.prefetch_after_prep else None)
         ev.wait()  # (the prep's done-callback may still be running on its pool thread)
         return r, box[0]
 
@@ -1165,7 +1167,8 @@ def run_epoch_bench(args, eng, world, rank, dev):
                                       "queue, combines deferred per window)" if args.epoch_coins == "ba"
                                       else "synthetic: one ThresholdSign per BA instance at epoch 2"),
                        "pipelined_drains": args.pipeline,
-                       "coin_prefetch": pf_on, "dec_preverify": not args.no_preverify,
+                       "coin_prefetch": pf_on, "coin_prefetch_start": "after_prep" if args.prefetch_after_prep else "epoch",
+                       "dec_preverify": not args.no_preverify, "dec_preverify_at": args.preverify_at,
                        "parallelism": "one node per rank x%d" % world,
                        "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},
             "outputs_ok": ok, "phase_ms": phases, "host_vs_gpu": host_gpu,

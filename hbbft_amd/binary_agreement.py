@@ -83,12 +83,13 @@ class BinaryAgreementCoin:
         sender stored in the incoming queue, or a current-epoch share stored by
         ThresholdSign.store_cached.  False: nothing changed (a fault, the share that completes the
         coin, an uncached verdict, or the verifier's shortcuts off) -- call handle_message."""
-        if not getattr(self.verifier, "shortcuts", False):
+        if not self.verifier.shortcuts:
             return False
-        if self.decision is not None or epoch < self.epoch:
+        be = self.epoch
+        if self.decision is not None or epoch < be:
             return True
-        if epoch > self.epoch:
-            if epoch > self.epoch + self.max_future_epochs or type(share) is not bytes:
+        if epoch > be:
+            if epoch > be + self.max_future_epochs or type(share) is not bytes:
                 return False
             q = self.incoming.get(epoch)
             if q is None:

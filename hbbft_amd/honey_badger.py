@@ -351,7 +351,7 @@ def _windows(verifier, msgs, window, instance, queue, hand, pipelined, limit, qu
 
 
 def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=False, slack=4, switch_interval=2e-4,
-              defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True, preverify_at="first_drain",
+              defer=True, raw=False, ba=None, coin_prefetch=None, preverify=True, preverify_at="start",
               after_prep=None, fast_paths=True):
     """Replay ``trace`` as node ``our``; returns an EpochResult.  ``window`` = messages per drain;
     ``pipelined`` overlaps each window's GPU drain with the host handling of the previous window;
@@ -365,8 +365,12 @@ def run_epoch(engine, keys, trace, window=6144, our=0, threads=0, pipelined=Fals
     one batch (DeserializeCiphertext faults, epoch_state.rs:377-381) and every window of share
     messages in one batch before it is queued (hbbft_amd.wire).
     ``preverify``: the contributions' ciphertext checks and the first t + 1 + slack decryption shares
-    of each are checked on a second engine while the coin phase runs (_dec_preverify), started after
-    the coin phase's first drain (``preverify_at="first_drain"``) or with the epoch (``"start"``).
+    of each are checked on a second engine while the coin phase runs (_dec_preverify), started with
+    the epoch (``preverify_at="start"``, round 5 default) or after the coin phase's first drain
+    (``"first_drain"``, round 4's).  Round 5's host decryption prep finishes in well under a millisecond,
+    so a pre-verification started at the first drain lands its GPU work on the coin phase's combines
+    and local engine calls (coin resolve + local 11 + 4 -> 21 ms); started with the epoch it is done
+    before they need the GPU: 19.7-19.9 -> 25.2-27.2 epochs/s (profiles/r05/c15_epoch_schedule.txt).
     ``after_prep``: called (from a host-pool thread) once this epoch's host decryption prep is done --
     a driver starts lower-priority host work there (the next epoch's coin prefetch) so that it does
     not share the host threads with the prep.
@@ -521,7 +525,7 @@ def _one_call(engine2, jobs):
 
 
 def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defer, raw, ba, coin_prefetch=None,
-               preverify=True, preverify_at="first_drain", after_prep=None, fast_paths=True):
+               preverify=True, preverify_at="start", after_prep=None, fast_paths=True):
     limit = None if slack is None else keys.t + 1 + slack
     res = EpochResult()
     # the background host work leaves two of the host threads to the flows and the drain worker
@@ -675,13 +679,19 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                     queued_n[pe] = c + 1
 
     def hand_window(batch, end):
-        shares = ba.shares
+        shares, fast = ba.shares, ver.shortcuts
         t_msgs = time.perf_counter()
         for m in batch:
             p, e, j = m
             b = bas[p]
-            # the common outcomes (ignored, future share queued, cached valid share stored) inside
-            # BinaryAgreementCoin.handle_fast; everything else through handle_message
+            # a message handle_message would ignore without a state change (decided instance, expired
+            # epoch, coin decided or pending: :245-252, _handle_coin) is skipped here -- most of an
+            # epoch's messages once its coins are done; the common transitions (future share queued,
+            # cached valid share stored) are BinaryAgreementCoin.handle_fast's, the rest handle_message's
+            if fast:
+                be = b.epoch
+                if b.decision is not None or e < be or (e == be and (b.coin_decided or b.pending is not None)):
+                    continue
             if b.handle_fast(j, e, shares[m]):
                 continue
             try:

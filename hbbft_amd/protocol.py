@@ -534,15 +534,20 @@ class ThresholdSign:
         storing it leaves the instance at <= t shares -- the share is stored, True is returned, and
         handle_message's result would have been an empty Step.  Otherwise (or with the verifier's
         shortcuts off) nothing changes and False is returned: handle_message decides."""
-        ni, rs, h = self.netinfo, self.received_shares, self.doc_hash
-        if (self.terminated or h is None or sender_id in rs or len(rs) >= ni.t or type(share) is not bytes
-                or not getattr(self.verifier, "shortcuts", False)):
+        rs, h, ver = self.received_shares, self.doc_hash, self.verifier
+        if self.terminated or h is None or sender_id in rs or type(share) is not bytes or not ver.shortcuts:
             return False
-        idx, pk = ni._index.get(sender_id), ni.pk_shares.get(sender_id)
-        d = self.verifier._sig.get(h)
-        if idx is None or type(pk) is not bytes or d is None or d.get((pk, share)) is not True:
+        ni = self.netinfo
+        if len(rs) >= ni.t:
             return False
-        self.verifier.lookups += 1  # the verdict consumed, as sig_valid counts it
+        d = ver._sig.get(h)
+        pk = ni.pk_shares.get(sender_id)
+        if d is None or type(pk) is not bytes or d.get((pk, share)) is not True:
+            return False
+        idx = ni._index.get(sender_id)
+        if idx is None:
+            return False
+        ver.lookups += 1  # the verdict consumed, as sig_valid counts it
         rs[sender_id] = (idx, share)
         return True
 
@@ -682,15 +687,20 @@ class ThresholdDecrypt:
         a VALID verdict for the share, and storing it leaves the instance at <= t shares -- stored,
         True returned (handle_message would return an empty Step).  Otherwise (or with the verifier's
         shortcuts off) nothing changes and False is returned: handle_message decides."""
-        ni, sh, ct = self.netinfo, self.shares, self.ciphertext
-        if (self.terminated or ct is None or sender_id in sh or len(sh) >= ni.t or type(share) is not bytes
-                or not getattr(self.verifier, "shortcuts", False)):
+        sh, ct, ver = self.shares, self.ciphertext, self.verifier
+        if self.terminated or ct is None or sender_id in sh or type(share) is not bytes or not ver.shortcuts:
             return False
-        idx, pk = ni._index.get(sender_id), ni.pk_shares.get(sender_id)
-        d = self.verifier._dec.get((ct.huv, ct.w))
-        if idx is None or type(pk) is not bytes or d is None or d.get((pk, share)) is not True:
+        ni = self.netinfo
+        if len(sh) >= ni.t:
             return False
-        self.verifier.lookups += 1  # the verdict consumed, as dec_valid counts it
+        d = ver._dec.get((ct.huv, ct.w))
+        pk = ni.pk_shares.get(sender_id)
+        if d is None or type(pk) is not bytes or d.get((pk, share)) is not True:
+            return False
+        idx = ni._index.get(sender_id)
+        if idx is None:
+            return False
+        ver.lookups += 1  # the verdict consumed, as dec_valid counts it
         sh[sender_id] = (idx, share)
         return True
 
