@@ -96,11 +96,13 @@ def test_config3_network_acks(engine):
 @pytest.mark.parametrize("t", [33, 5, 1])
 def test_ack_finite_differences_match_horner(engine, t):
     """Round 5: the one-lane Ack path checks the acks of a row whose y form a dense run by finite
-    differences (hbl::bivar_fd: Horner at t + 1 points, the forward-difference table, t G1 additions
-    per further y).  Rows of every shape -- a node's full run y = 1..100, runs with gaps, a run not
-    starting at 1, duplicated y, a run of exactly 2 (t + 1) acks, a longer run, and sparse rows that
-    stay on Horner -- with 1/11 tampered values: FD verdicts == Horner-only == lane quads == the
-    construction, plus C-oracle samples (BivarCommitment::evaluate == g1 * val, sync_key_gen.rs:542)."""
+    differences (hbl::bivar_fd: the forward-difference table at y0 seeded from the row -- y0 = 0, or
+    the run's first y when it starts beyond t + 1 -- then t G1 additions per further y).  Rows of every
+    shape -- a node's full run y = 1..100, runs with gaps, a run starting at 50 (the general seed),
+    duplicated y, a run of exactly 2 (t + 1) acks, a longer run, sparse rows and a heavily duplicated
+    short run (enough acks, too short a span for the seed's two tables: Horner at t = 33) -- with 1/11
+    tampered values: FD verdicts == Horner-only == lane quads == the construction, plus C-oracle
+    samples (BivarCommitment::evaluate == g1 * val, sync_key_gen.rs:542)."""
     from hbbft_amd import hoststage
     rng = random.Random(700 + t)
     T1 = t + 1
@@ -116,7 +118,8 @@ def test_ack_finite_differences_match_horner(engine, t):
             (2, 1, sorted(rng.sample(range(1, 1000), 30))),
             (3, 1, list(range(1, 2 * T1 + 1))),
             (4, 7, list(range(1, 201))),
-            (5, 3, list(range(1, T1 + 2)))]
+            (5, 3, list(range(1, T1 + 2))),
+            (5, 5, [y for y in range(1, T1 + 8) for _ in range(3)])]
     acks = [(p, x, y) for p, x, ys in runs for y in ys]
     rng.shuffle(acks)
     # vals: row(x) of part p is the polynomial in y with coefficients sum_i c(i, j) x^i
