@@ -105,3 +105,51 @@ def test_reordering_attack_fake_coin(seed):
                                     random.Random(seed))
     outs = [net.nodes[i].outputs for i in range(1, ba_mitm.NUM_NODES)]
     assert all(len(o) == 1 for o in outs) and len({o[0] for o in outs}) == 1
+
+
+class RandomFaultyAdversary(ReorderingAdversary):
+    """Faulty nodes ignore the protocol: every message to one of them is answered with a random
+    Binary Agreement message (BVal / Aux / Conf / Term with a random value, for the current or a
+    nearby epoch) to a random correct node; deliveries are reordered at random.  Correct nodes must
+    still agree, terminate, keep validity among the correct inputs, and blame only faulty nodes."""
+
+    def __init__(self, rng):
+        self.rng = rng
+
+    def tamper(self, net, msg, rng):
+        from hbbft_amd.protocol import Step
+        from hbbft_amd.binary_agreement import BOTH, FALSE, TRUE
+        from .virtual_net import NetMessage
+        r = self.rng
+        epoch = max(0, msg.payload[0] + r.choice((-1, 0, 0, 1)))
+        kind = r.choice(("BVal", "Aux", "Conf", "Term"))
+        val = r.choice((FALSE, TRUE, BOTH)) if kind == "Conf" else r.random() < 0.5
+        good = [n for n, nd in net.nodes.items() if not nd.faulty]
+        net.inject_message(False, NetMessage(msg.to, (epoch, (kind, val)), r.choice(good)))
+        return Step()
+
+
+@pytest.mark.parametrize("n,faulty,inp,seed", [(4, 1, True, 41), (7, 2, False, 42), (7, 2, None, 43),
+                                                (10, 3, None, 44)])
+def test_binary_agreement_random_faulty_nodes(n, faulty, inp, seed):
+    """tests/binary_agreement.rs's properties with faulty nodes that send random BA messages: the
+    correct nodes decide one value, the correct nodes' common input when they share one, and every
+    fault a correct node records names a faulty node (VirtualNet raises otherwise)."""
+    rng = random.Random(seed)
+    net = VirtualNet(range(n), faulty, lambda nid, f: BinaryAgreement(fake_netinfo(n)(nid), BatchVerifier(FakeEngine()),
+                                                                      BinaryAgreement.session_bytes(0)),
+                     adversary=RandomFaultyAdversary(random.Random(seed + 1)), message_limit=10000 * n)
+    correct = [nid for nid, nd in net.nodes.items() if not nd.faulty]
+    for nid in correct:
+        net.send_input(nid, inp if inp is not None else rng.random() < 0.5)
+    # faulty nodes start the noise with one message each
+    for nid, nd in net.nodes.items():
+        if nd.faulty:
+            net.inject_message(False, ba_mitm.NetMessage(nid, (0, ("BVal", True)), correct[0]))
+    while not all(net.nodes[i].algorithm.terminated() for i in correct):
+        net.crank_expect(rng)
+    outs = [net.nodes[i].outputs for i in correct]
+    assert all(len(o) == 1 for o in outs) and len({o[0] for o in outs}) == 1
+    if inp is not None:
+        assert outs[0] == [inp]
+    assert all(f.node_id < faulty for i in correct for f in net.nodes[i].faults)
