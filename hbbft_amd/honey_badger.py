@@ -494,7 +494,37 @@ def _dec_preverify(engine2, keys, trace, prep, limit):
         pre.queue_dec(keys.pks[j], trace.dec_shares[(p, j)], huv_of[p], trace.cts[p][2])
     t0 = time.perf_counter()
     out = _one_call(engine2, pre._take_jobs())
-    return out, t_prep, time.perf_counter() - t0
+    # speculative decryption combines on the same engine: per valid ciphertext, the first t + 1 shares
+    # (arrival order) whose verdicts are valid.  Any t + 1 valid shares of a ciphertext interpolate to
+    # U * msk, so the deferred G1 combine of its ThresholdDecrypt (threshold_decrypt.rs:242-250) takes
+    # this point unchanged (BatchVerifier._spec_g1) and leaves the decrypt phase's critical path
+    spec = {}
+    ok = {}
+    for kind, ks, v in out:
+        for k, b in zip(ks, v):
+            ok[(kind, k)] = bool(b)
+    t = keys.t
+    sel = {}
+    for p, j in trace.dec_msgs:
+        if p not in huv_of:
+            continue
+        u, _, w = trace.cts[p]
+        if not ok.get(("ct", (u, w, huv_of[p])), False):
+            continue
+        got = sel.setdefault(p, {})
+        if len(got) > t or j in got:
+            continue
+        sh = trace.dec_shares[(p, j)]
+        if ok.get(("dec", (keys.pks[j], sh, huv_of[p], w)), False):
+            got[j] = sh
+    ps = [p for p in sorted(sel) if len(sel[p]) == t + 1]
+    if ps:
+        idx = [sorted(sel[p]) for p in ps]
+        pts, st = engine2.interpolate_g1(t, idx, [[sel[p][j] for j in ix] for p, ix in zip(ps, idx)])
+        for p, pt, s_ in zip(ps, pts, st):
+            if s_ == 0:
+                spec[(huv_of[p], trace.cts[p][2])] = pt
+    return (out, spec), t_prep, time.perf_counter() - t0
 
 
 def _one_call(engine2, jobs):
@@ -819,12 +849,13 @@ def _decrypt_and_output(engine, keys, trace, ver, window, our, threads, pipeline
     td = {p: ThresholdDecrypt(ni_dec, ver) for p in ps}
     if dec_pre is not None:  # the verdicts checked beside the coin phase (_dec_preverify) into the cache
         t1 = time.perf_counter()
-        pre, t_prep, t_eng = dec_pre.result()
+        (pre, spec), t_prep, t_eng = dec_pre.result()
         res.timing["decrypt_pre_prep"], res.timing["decrypt_pre_engine"] = t_prep, t_eng
         t2 = time.perf_counter()
         ver.wait_s += t2 - t1
         res.timing["decrypt_pre_wait"] = t2 - t1
         ver._store(pre)
+        ver.add_speculative_g1(spec)
         res.timing["decrypt_pre_store"] = time.perf_counter() - t2
     for p in ps:
         ver.queue_ct(cts[p])  # (our own decryption share is not verified, threshold_decrypt.rs:167)

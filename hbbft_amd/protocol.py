@@ -117,10 +117,10 @@ class Deferred:
     optimistically; when it failed, the reference would have returned ``Err`` from the call that
     triggered it and (ThresholdSign) stayed open, so the driver replays that instance's inputs with
     immediate combines (honey_badger.run_epoch) -- the Steps and errors are then the reference's."""
-    __slots__ = ("key", "result", "data")
+    __slots__ = ("key", "result", "data", "tag")
 
     def __init__(self, key, data=None):
-        self.key, self.result, self.data = key, None, data
+        self.key, self.result, self.data, self.tag = key, None, data, None
 
     @property
     def ok(self):
@@ -152,6 +152,10 @@ class BatchVerifier:
         self.shortcuts = True
         self._docs = {}
         self._rec_g2, self._rec_g1 = [], []
+        # speculative G1 combines (honey_badger._dec_preverify): ciphertext key (H_uv, W) -> U * msk from
+        # t + 1 shares whose verdicts are valid; any t + 1 valid decryption shares of one ciphertext
+        # interpolate to that same point, so a deferred combine of the ciphertext takes it unchanged
+        self._spec_g1 = {}
         self._released = set()  # instances released since the last drain was stored
         self._open = {}         # instance key -> number of running instances that use it
         self._inflight = 0      # drain_async calls not yet committed
@@ -228,6 +232,10 @@ class BatchVerifier:
                 d.result = (o, s_, bool(vv))
         groups = {}
         for d in self._rec_g1:
+            pt = self._spec_g1.get(d.tag) if d.tag is not None else None
+            if pt is not None and len(set(d.key[1])) == len(d.key[1]):  # (a repeated index: compute)
+                d.result = (pt, 0)
+                continue
             groups.setdefault(d.key[0], []).append(d)
         for t, ds in groups.items():
             out, st = self.ceng.interpolate_g1(t, [list(d.key[1]) for d in ds], [list(d.key[2]) for d in ds])
@@ -238,6 +246,10 @@ class BatchVerifier:
         failed = [d for d in self._rec_g2 + self._rec_g1 if not d.ok]
         self._rec_g2, self._rec_g1 = [], []
         return failed
+
+    def add_speculative_g1(self, points):
+        """{(H_uv, W): G1 point} combined early from verified decryption shares (see _spec_g1)."""
+        self._spec_g1.update(points)
 
     # Instances are reference-counted by their key (document hash; (H_uv, W) for a ciphertext):
     # two running instances may share one (a Byzantine proposer can copy another's ciphertext, two
@@ -760,6 +772,7 @@ class ThresholdDecrypt:
             raise ProtocolError("Decryption", "DuplicateEntry")
         if isinstance(g, Deferred):
             g.data = self.ciphertext.v
+            g.tag = (self.ciphertext.huv, self.ciphertext.w)
             return step.with_output(g)
         return step.with_output(xor_with_hash(g, self.ciphertext.v))
 
