@@ -25,6 +25,7 @@ The CPU comparison is the reference-equivalent work: the checks the flows actual
 combines, timed on the C restatement by bench.py (oracle use stays in bench/tests).
 """
 import concurrent.futures
+import os
 import random
 import struct
 import sys
@@ -495,35 +496,38 @@ def _dec_preverify(engine2, keys, trace, prep, limit):
     t0 = time.perf_counter()
     out = _one_call(engine2, pre._take_jobs())
     # speculative decryption combines on the same engine: per valid ciphertext, the first t + 1 shares
-    # (arrival order) whose verdicts are valid.  Any t + 1 valid shares of a ciphertext interpolate to
-    # U * msk, so the deferred G1 combine of its ThresholdDecrypt (threshold_decrypt.rs:242-250) takes
-    # this point unchanged (BatchVerifier._spec_g1) and leaves the decrypt phase's critical path
+    # (arrival order: the order they were queued) whose verdicts are valid.  Any t + 1 valid shares of
+    # a ciphertext interpolate to U * msk, so the deferred G1 combine of its ThresholdDecrypt
+    # (threshold_decrypt.rs:242-250) takes this point unchanged (BatchVerifier._spec_g1) and leaves
+    # the decrypt phase's critical path (HBH_EPOCH_SPEC_G1=0: off)
     spec = {}
-    ok = {}
-    for kind, ks, v in out:
-        for k, b in zip(ks, v):
-            ok[(kind, k)] = bool(b)
-    t = keys.t
-    sel = {}
-    for p, j in trace.dec_msgs:
-        if p not in huv_of:
-            continue
-        u, _, w = trace.cts[p]
-        if not ok.get(("ct", (u, w, huv_of[p])), False):
-            continue
-        got = sel.setdefault(p, {})
-        if len(got) > t or j in got:
-            continue
-        sh = trace.dec_shares[(p, j)]
-        if ok.get(("dec", (keys.pks[j], sh, huv_of[p], w)), False):
-            got[j] = sh
-    ps = [p for p in sorted(sel) if len(sel[p]) == t + 1]
-    if ps:
-        idx = [sorted(sel[p]) for p in ps]
-        pts, st = engine2.interpolate_g1(t, idx, [[sel[p][j] for j in ix] for p, ix in zip(ps, idx)])
-        for p, pt, s_ in zip(ps, pts, st):
-            if s_ == 0:
-                spec[(huv_of[p], trace.cts[p][2])] = pt
+    if os.environ.get("HBH_EPOCH_SPEC_G1", "1") != "0":
+        by = {kind: (ks, v) for kind, ks, v in out}
+        cks, cv = by.get("ct", ((), b""))
+        dks, dv = by.get("dec", ((), b""))
+        valid_ct = {(k[2], k[1]) for k, ok in zip(cks, cv) if ok}
+        pk_idx = {pk: j for j, pk in keys.pks.items()}
+        t = keys.t
+        sel = {}
+        for k, ok in zip(dks, dv):  # k = (pk, share, H_uv, W)
+            if not ok:
+                continue
+            c = (k[2], k[3])
+            if c not in valid_ct:
+                continue
+            got = sel.get(c)
+            if got is None:
+                got = sel[c] = {}
+            elif len(got) > t:
+                continue
+            j = pk_idx.get(k[0])
+            if j is not None and j not in got:
+                got[j] = k[1]
+        cs = [c for c in sel if len(sel[c]) == t + 1]
+        if cs:
+            idx = [sorted(sel[c]) for c in cs]
+            pts, st = engine2.interpolate_g1(t, idx, [[sel[c][j] for j in ix] for c, ix in zip(cs, idx)])
+            spec = {c: pt for c, pt, s_ in zip(cs, pts, st) if s_ == 0}
     return (out, spec), t_prep, time.perf_counter() - t0
 
 
