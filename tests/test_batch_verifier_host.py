@@ -176,3 +176,33 @@ def test_engine_wait_is_accounted():
     w0 = ver.wait_s
     ver.commit(ver.drain_async())
     assert ver.async_s >= 0.015 and ver.wait_s >= w0
+
+
+def test_speculative_g1_combines_serve_deferred_decryptions():
+    """BatchVerifier._spec_g1 (round 5, honey_badger._dec_preverify): a deferred G1 combine tagged with a
+    ciphertext key whose point was combined early takes that point without an engine call; untagged
+    ones, keys without a point, and a set with a repeated index go to the engine."""
+    from hbbft_amd.protocol import Deferred
+
+    class G1Engine(FakeEngine):
+        def interpolate_g1(self, t, idx, pts):
+            self.calls.append(("g1", len(idx), threading.current_thread().name))
+            return [b"engine" + bytes(len(i)) for i in idx], [0] * len(idx)
+
+    eng = G1Engine()
+    ver = BatchVerifier(eng)
+    ver.recording = True
+    ver.add_speculative_g1({(b"huv1", b"w1"): b"spec-point"})
+    d1, _ = ver.interpolate_g1(1, [0, 1], [b"a", b"b"])
+    d1.tag = (b"huv1", b"w1")
+    d2, _ = ver.interpolate_g1(1, [2, 3], [b"c", b"d"])
+    d2.tag = (b"huv2", b"w2")                      # no speculative point for this ciphertext
+    d3, _ = ver.interpolate_g1(1, [4, 4], [b"e", b"e"])
+    d3.tag = (b"huv1", b"w1")                      # repeated index: the engine decides (DuplicateEntry)
+    d4, _ = ver.interpolate_g1(1, [5, 6], [b"f", b"g"])  # untagged
+    assert all(isinstance(d, Deferred) for d in (d1, d2, d3, d4))
+    ver.flush_combines()
+    assert d1.result == (b"spec-point", 0)
+    assert d2.result[0].startswith(b"engine") and d3.result[0].startswith(b"engine")
+    assert d4.result[0].startswith(b"engine")
+    assert [c[:2] for c in eng.calls] == [("g1", 3)]
