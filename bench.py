@@ -419,10 +419,20 @@ def g2_compress_abi(b):
     return bytes(e)
 
 
+def g1_compress_abi(b):
+    """ABI G1 point -> 48-byte compressed wire encoding (pairing 0.14 G1Compressed)."""
+    if not any(b):
+        return bytes([0xC0]) + bytes(47)
+    x, y = (int.from_bytes(b[o:o + 48], "little") for o in (0, 48))
+    e = bytearray(x.to_bytes(48, "big"))
+    e[0] |= 0x80 | (0x20 if y > (P_FIELD - y) % P_FIELD else 0)
+    return bytes(e)
+
+
 def decode_rate(eng, w, n):
-    """Wire decoding of the batch's n signature shares: hbh_g2_decompress rate
-    host-to-host (PCIe + host flag parsing included) and device-only; decoded bytes must equal the
-    shares the workload generated."""
+    """Wire decoding of the batch's n signature shares (G2) and n public-key-share encodings (G1)
+    (SURVEY §8f f2): hbh_g2_decompress rate host-to-host (PCIe + host flag parsing included) and
+    device-only, and the device-only G1 rate; decoded bytes must equal the generated points."""
     from hbbft_amd._lib import STAGE_CURVE
     sig = w.sig_batch[:n * 192]
     encs = b"".join(g2_compress_abi(sig[i * 192:(i + 1) * 192]) for i in range(n))
@@ -434,7 +444,77 @@ def decode_rate(eng, w, n):
     dev_ms = eng.stage_time(STAGE_CURVE)[0]
     eng.set_profiling(False)
     assert all(ok) and b"".join(pts) == sig, "G2 decoding differs from the generated shares"
-    return n / host_s, n / (dev_ms / 1e3)
+    pk = w.pk_batch[:n * 96]
+    pk_enc = {}
+    encs1 = b"".join(pk_enc.setdefault(pk[i * 96:(i + 1) * 96], g1_compress_abi(pk[i * 96:(i + 1) * 96]))
+                     for i in range(n))
+    eng.set_profiling(True)
+    pts1, ok1 = eng.g1_decompress(encs1)
+    dev1_ms = eng.stage_time(STAGE_CURVE)[0]
+    eng.set_profiling(False)
+    assert all(ok1) and b"".join(pts1) == pk, "G1 decoding differs from the generated keys"
+    return {"g2_decode_per_s": n / host_s, "g2_decode_per_s_device": n / (dev_ms / 1e3),
+            "g2_decode_ms_device": dev_ms, "g1_decode_per_s_device": n / (dev1_ms / 1e3),
+            "g1_decode_ms_device": dev1_ms, "decode_points": n}
+
+
+def from_wire(eng, w, n, streams, steps, warmup, world, dev, d_pk, d_hs, d_di, to_dev):
+    """The whole node from wire bytes: each step takes the batch's n signature
+    shares as the 96-byte compressed encodings a node receives (threshold_sign::Message,
+    src/threshold_sign.rs:73; the Message's bincode framing is host work, wire.py) already in HBM,
+    decodes them on the device (k_wire_parse + k_g2_decompress: flags, square root, subgroup test,
+    hbh_g2_decompress_dev) and verifies them (verify_pairing_eq_dev), consecutive batches on
+    alternating streams as the device-resident line.  A share that fails to decode is a
+    DeserializeMessage fault in the reference, never a verdict; every encoding here decodes and
+    the decoded bytes and verdicts are checked after the timed steps."""
+    from hbbft_amd import workcount
+    from hbbft_amd._lib import STAGE_CURVE, STAGE_PAIRING
+    sig = w.sig_batch[:n * 192]
+    encs = b"".join(g2_compress_abi(sig[i * 192:(i + 1) * 192]) for i in range(n))
+    d_enc = to_dev(encs)
+    d_sg = [torch.empty(n * 192, dtype=torch.uint8, device=dev) for _ in streams]
+    d_ok = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in streams]
+    d_v = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in streams]
+    nh = len(w.hashes)
+
+    def step(k=0):
+        j = k % len(streams)
+        cs = streams[j].cuda_stream
+        eng.g2_decompress_dev(cs, n, d_enc.data_ptr(), d_sg[j].data_ptr(), d_ok[j].data_ptr())
+        eng.verify_pairing_eq_dev(cs, n, d_pk.data_ptr(), d_hs.data_ptr(), nh, d_di.data_ptr(), None,
+                                  d_sg[j].data_ptr(), n, None, d_v[j].data_ptr())
+
+    def outputs_ok(nbuf=None):
+        return all(bool(d_ok[j].cpu().numpy().all()) and bool((d_v[j].cpu().numpy() == w.expected).all())
+                   and d_sg[j].cpu().numpy().tobytes() == sig for j in range(len(streams))[:nbuf])
+
+    for k in range(len(streams)):
+        step(k)
+    torch.cuda.synchronize(dev)
+    ok = outputs_ok()
+    for k in range(warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    for j in range(len(streams)):
+        d_ok[j].zero_()
+        d_v[j].zero_()
+        d_sg[j].zero_()
+    ms = timed_steps(step, streams, steps, world, dev)
+    ok = ok and outputs_ok(min(steps, len(streams)))
+    eng.set_profiling(True)
+    for _ in range(3):
+        step(0)
+    torch.cuda.synchronize(dev)
+    dec_ms, dec_n = eng.stage_time(STAGE_CURVE)
+    pair_ms, pair_n = eng.stage_time(STAGE_PAIRING)
+    eng.set_profiling(False)
+    dec_avg = dec_ms / max(dec_n, 1)
+    return {"value": n * world / (ms / 1e3), "unit": "shares/s", "ms_per_step": ms, "steps": steps,
+            "outputs_ok": ok, "decode_ms_isolated": dec_avg, "verify_ms_isolated": pair_ms / max(pair_n, 1),
+            "kernels": [roofline_entry("hb::k_g2_decompress", dec_n, dec_avg, n, workcount.WIRE_G2_DECODE,
+                                       "compressed G2 point (flags, sqrt, subgroup)",
+                                       n / 64 / 1024, source="sign")],
+            "input": "%d compressed 96-byte signature shares in HBM per step (%d documents)" % (n, nh)}
 
 
 def main():
@@ -445,6 +525,11 @@ def main():
     ap.add_argument("--batch", type=int, default=NDOCS * N_NODES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-combine", action="store_true")
+    ap.add_argument("--no-wire", action="store_true",
+                    help="sign workload: skip the whole-node-from-wire-bytes line (decode + verify per step)")
+    ap.add_argument("--from-wire", action="store_true",
+                    help="sign workload: the line's value is the whole node from wire bytes (compressed shares "
+                         "decoded on the device inside every timed step) instead of device-resident points")
     ap.add_argument("--no-node-round", action="store_true",
                     help="dkg workload: skip the one-node SyncKeyGen round (node_round)")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
@@ -472,6 +557,9 @@ def main():
     ap.add_argument("--pipeline", action="store_true",
                     help="epoch workload: drain window k on a worker thread while the flows handle window k - 1 "
                          "(measured slower than serial drains on MI355X, profiles/r04/c6_epoch_ab.txt)")
+    ap.add_argument("--raw", action="store_true",
+                    help="epoch workload: the node receives bincode bytes (contributions, coin-share and "
+                         "decryption-share messages), decoded on the device per window inside the timed epoch")
     ap.add_argument("--no-preverify", action="store_true",
                     help="epoch workload: no decryption-share pre-verification beside the coin phase")
     ap.add_argument("--no-prefetch", action="store_true",
@@ -560,6 +648,11 @@ def main():
     per_rank = gather_per_rank({"rank": rank, "device": local, "kernel_ms": pair_ms / max(pair_n, 1),
                                 "ms_per_step": ms_step, "verdicts_ok": ok}, world)
     ok = all(r["verdicts_ok"] for r in per_rank)
+    wire = None
+    if args.from_wire or not args.no_wire:
+        wire = from_wire(eng, w, n, streams, max(2, args.steps if args.from_wire else min(args.steps, 5)),
+                         args.warmup, world, dev, d_pk, d_hs, d_di, to_dev)
+        ok = ok and wire["outputs_ok"]
 
     if rank == 0:
         kern_ms = pair_ms / max(pair_n, 1)
@@ -588,14 +681,18 @@ def main():
                                   "average launch time of isolated single-stream launches (the throughput value alternates two "
                                   "streams); peak = measured MAD rate at 8 waves/SIMD"),
         }
+        if wire is not None:
+            out["whole_node_from_wire"] = wire
+            if args.from_wire:
+                out["value"], out["ms_per_step"] = wire["value"], wire["ms_per_step"]
+                out["roofline"]["kernels"] = out["roofline"]["kernels"] + wire["kernels"]
+                out["config"]["workload"] += ", from compressed wire bytes (decode + verify per step)"
         if not args.no_combine:
             lat, rate, dev_rate = combine_latency(eng, w)
             out["combine_latency_ms"] = lat
             out["combines_per_s_batched"] = rate          # host-to-host, 1,024 combines in one call
             out["combines_per_s_batched_device"] = dev_rate  # k_interp_endo time only
-            dec_host, dec_dev = decode_rate(eng, w, n)
-            out["g2_decode_per_s"] = dec_host            # hbh_g2_decompress, host-to-host
-            out["g2_decode_per_s_device"] = dec_dev      # k_g2_decompress time only
+            out.update(decode_rate(eng, w, n))  # hbh_g2/g1_decompress: host-to-host and kernel-only rates
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(w)
         print(json.dumps(out), flush=True)
@@ -1065,6 +1162,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
     if args.epoch_coins == "ba":  # coins from Binary Agreement instances (future-epoch queue, per-window combines)
         for tr in traces:
             tr.with_ba(eng, rng, extra=0.0)
+    if args.raw:  # the bincode bytes the node receives (hbbft_amd.wire); decoding is inside the timed epochs
+        for tr in traces:
+            tr.serialize()
     log("generated %d epoch traces in %.1f s" % (len(traces), time.time() - t0))
     ok = True
     # each epoch starts the next one's coin prefetch (honey_badger.prefetch_coins: hash_g2 and our
@@ -1089,7 +1189,7 @@ def run_epoch_bench(args, eng, world, rank, dev):
 
         if not args.prefetch_after_prep:
             start_next()
-        r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf,
+        r = run_epoch(eng, keys, tr, window=args.window, pipelined=args.pipeline, coin_prefetch=pf, raw=args.raw,
                       preverify=not args.no_preverify, preverify_at=args.preverify_at,
                       after_prep=start_next if args.prefetch_after_prep else None)
         ev.wait()  # (the prep's done-callback may still be running on its pool thread)
@@ -1167,8 +1267,9 @@ def run_epoch_bench(args, eng, world, rank, dev):
                                       "queue, combines deferred per window)" if args.epoch_coins == "ba"
                                       else "synthetic: one ThresholdSign per BA instance at epoch 2"),
                        "pipelined_drains": args.pipeline,
+                       "from_wire_bytes": args.raw,
                        "coin_prefetch": pf_on, "coin_prefetch_start": "after_prep" if args.prefetch_after_prep else "epoch",
-                       "dec_preverify": not args.no_preverify, "dec_preverify_at": args.preverify_at,
+                       "dec_preverify": not args.no_preverify and not args.raw, "dec_preverify_at": args.preverify_at,
                        "parallelism": "one node per rank x%d" % world,
                        "timing": "host wall time of run_epoch (flows + host stage + engine calls)"},
             "outputs_ok": ok, "phase_ms": phases, "host_vs_gpu": host_gpu,

@@ -111,6 +111,13 @@ struct hbh_engine {
   hipEvent_t slot_done[2] = {nullptr, nullptr};
   int slot = 0;
   DevBuf ptab[2][2], pinf[2][2];
+  // Device-pointer point decoding (hbh_g*_decompress_dev) alternates between two staging slots of
+  // its own (wire words + flags), with its own completion events: a node's decode of one batch then
+  // runs beside the previous batch's verify on another stream (the whole-node sign line, bench.py
+  // --from-wire) instead of waiting for it.  It touches no other engine workspace.
+  hipEvent_t wire_done[2] = {nullptr, nullptr};
+  int wire_slot = 0;
+  DevBuf wire_w[2], wire_f[2];
   // host staging of combine digits (kept alive until the call's stream synchronises)
   std::vector<uint64_t> h_digits;
   std::vector<int> h_status;
@@ -357,6 +364,8 @@ int hbh_engine_create(int device, hbh_engine** out) {
   for (int k = 0; k < 2 && err == hipSuccess; k++) {
     err = hipEventCreateWithFlags(&e->slot_done[k], hipEventDisableTiming);
     if (err == hipSuccess) err = hipEventRecord(e->slot_done[k], e->stream);
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&e->wire_done[k], hipEventDisableTiming);
+    if (err == hipSuccess) err = hipEventRecord(e->wire_done[k], e->stream);
   }
   if (err != hipSuccess) {
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -380,13 +389,16 @@ int hbh_engine_destroy(hbh_engine* e) {
   (void)hipEventSynchronize(e->done);
   for (hipEvent_t ev : e->slot_done)
     if (ev) (void)hipEventSynchronize(ev);
+  for (hipEvent_t ev : e->wire_done)
+    if (ev) (void)hipEventSynchronize(ev);
   (void)hipStreamSynchronize(e->stream);
   if (e->side) (void)hipStreamSynchronize(e->side);
   e->timer.clear();
   for (DevBuf* b : {&e->work, &e->status, &e->fbtab, &e->ipart, &e->in_p1, &e->in_q1, &e->in_i1, &e->in_p2, &e->in_q2, &e->in_i2, &e->out_v,
                     &e->in_a, &e->in_b, &e->in_c, &e->in_d, &e->out_x, &e->ptab[0][0], &e->ptab[0][1], &e->ptab[1][0],
                     &e->ptab[1][1], &e->pinf[0][0], &e->pinf[0][1], &e->pinf[1][0], &e->pinf[1][1], &e->fval, &e->split_in,
-                    &e->split_out, &e->tree_cnt, &e->fd_e, &e->fd_meta, &e->fb16})
+                    &e->split_out, &e->tree_cnt, &e->fd_e, &e->fd_meta, &e->fb16, &e->wire_w[0], &e->wire_w[1],
+                    &e->wire_f[0], &e->wire_f[1]})
     b->release();
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   (void)hipEventDestroy(e->done);
@@ -396,6 +408,8 @@ int hbh_engine_destroy(hbh_engine* e) {
     (void)hipStreamDestroy(e->side);
   }
   for (hipEvent_t ev : e->slot_done)
+    if (ev) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->wire_done)
     if (ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
   delete e;
@@ -1399,18 +1413,24 @@ int run_decompress_dev(hbh_engine* e, void* stream, size_t n, const uint8_t* d_i
   std::lock_guard<std::mutex> lk(e->mu);
   HBH_CHECK(hipSetDevice(e->device));
   hipStream_t s = dev_stream(e, stream);
-  int rc = begin_call(e, s);
-  if (rc) return rc;
-  HBH_CHECK(e->in_a.ensure(n * 12 * nfe * 4));
-  HBH_CHECK(e->in_b.ensure(n));
+  // a staging slot of its own: wait for the last general call and this slot's previous user only
+  const int slot = e->wire_slot;
+  e->wire_slot ^= 1;
+  HBH_CHECK(hipStreamWaitEvent(s, e->done, 0));
+  HBH_CHECK(hipStreamWaitEvent(s, e->wire_done[slot], 0));
+  HBH_CHECK(e->wire_w[slot].ensure(n * 12 * nfe * 4));
+  HBH_CHECK(e->wire_f[slot].ensure(n));
+  uint32_t* xw = (uint32_t*)e->wire_w[slot].p;
+  uint8_t* fl = (uint8_t*)e->wire_f[slot].p;
   hipEvent_t tm = e->timer.begin(s, HBH_STAGE_CURVE, e->profiling);
-  HBH_CHECK(hbl::wire_parse(s, (int)n, nfe, d_in, (uint32_t*)e->in_a.p, (uint8_t*)e->in_b.p));
+  HBH_CHECK(hbl::wire_parse(s, (int)n, nfe, d_in, xw, fl));
   if (g2)
-    HBH_CHECK(hbl::g2_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, d_out, d_ok));
+    HBH_CHECK(hbl::g2_decompress(s, (int)n, xw, fl, d_out, d_ok));
   else
-    HBH_CHECK(hbl::g1_decompress(s, (int)n, (const uint32_t*)e->in_a.p, (const uint8_t*)e->in_b.p, d_out, d_ok));
+    HBH_CHECK(hbl::g1_decompress(s, (int)n, xw, fl, d_out, d_ok));
   e->timer.end(s, tm);
-  return end_call(e, s);
+  HBH_CHECK(hipEventRecord(e->wire_done[slot], s));
+  return HBH_OK;
 }
 }  // namespace
 

@@ -1,32 +1,16 @@
 // Wire-format parsing on the GPU: pairing 0.14 G1Compressed / G2Compressed
 // ::into_affine for batches of compressed points (public keys, decryption shares, ciphertext U in
 // G1; signature shares, signatures, ciphertext W in G2) -- the square root that recovers y, the
-// sign choice and the prime-order-subgroup check.  The host does
+// sign choice and the prime-order-subgroup check (round 6: norm-method square root over one
+// windowed exponentiation chain, endomorphism subgroup tests).  The host does
 // the byte-level flag checks and the big-endian -> little-endian word reversal (wire.hpp).
 #include <hip/hip_runtime.h>
 
 #include "curve.hpp"
-#include "fr.hpp"
 #include "wire.hpp"
+#include "sqrt_chain.inc"
 
 namespace hb {
-
-// (p + 1) / 4 as 32-bit words (p = 3 mod 4, so a^((p+1)/4) is a square root of a square a)
-__device__ __forceinline__ void sqrt_exp_words(uint32_t e[12]) {
-  uint32_t w[12];
-  for (int i = 0; i < 12; i++) w[i] = PM2_W[i];
-  w[0] += 3;  // p - 2 + 3 = p + 1 (no carry: the low word of p - 2 is 0xffffaaa9)
-  for (int i = 0; i < 12; i++) e[i] = (w[i] >> 2) | (i < 11 ? (w[i + 1] << 30) : 0u);
-}
-
-__device__ __forceinline__ Fp fp_pow_words(const Fp& a, const uint32_t e[12]) {
-  Fp r = fp_one();
-  for (int i = 12 * 32 - 1; i >= 0; i--) {
-    r = fp_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1) r = fp_mul(r, a);
-  }
-  return r;
-}
 
 // canonical words a > b
 __device__ __forceinline__ bool words_gt(const uint32_t* a, const uint32_t* b, int n) {
@@ -35,6 +19,71 @@ __device__ __forceinline__ bool words_gt(const uint32_t* a, const uint32_t* b, i
   return false;
 }
 
+// ---------------------------------------------------------------------------- subgroup membership
+// Endomorphism tests instead of r * P == O (255-bit double-and-add):
+//   G1: P in G1  <=>  phi(P) == [-x^2] P,  phi(x, y) = (beta x, y)            (Scott, eprint 2021/1130)
+//   G2: P in G2  <=>  psi(P) == [x] P,     psi the untwist-Frobenius-twist map  (same note)
+// with x = -|x| = -0xd201000000010000.  Exact on the whole curve, not only on likely inputs: on the
+// l-power torsion of any prime l != r, phi + [x^2] has determinant x^4 - x^2 + 1 = r (phi^2 + phi +
+// 1 = 0) and psi - [x] has x^2 - t x + p = p - x = h1 r (psi^2 - t psi + p = 0, t = x + 1), units mod
+// every prime of h1 and h2, so neither map vanishes on a point outside the r-torsion
+// (tests/test_subgroup_criteria.py).  [|x|] is 63 doublings + 5 additions (|x| has 6 set bits), so
+// G2 pays 68 group operations instead of ~383 and G1 two such chains.  Both criteria are
+// equalities of points, so a non-subgroup point whose chain hits an exceptional addition (P = +-Q,
+// O) is handled by the group law's explicit cases (curve.hpp).  tests/test_gpu_wire_subgroup.py
+// pins accept / reject against the oracle's r * P test on random on-curve points and on points of
+// every prime order dividing the cofactors.
+
+// [|x|] P for an affine P (not infinity): double-and-add over the constant |x|, one mixed addition
+// per set bit.  Not unrolled: the loop control is uniform and one copy stays in the I-cache.
+template <class F>
+__device__ __forceinline__ Jac<F> mul_absx_affine(const F& x, const F& y) {
+  Jac<F> acc = jac_from_affine(x, y, false);
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add_affine(acc, x, y);
+  }
+  return acc;
+}
+
+template <class F>
+__device__ __forceinline__ Jac<F> mul_absx_jac(const Jac<F>& p) {
+  Jac<F> acc = p;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((X_ABS >> i) & 1) acc = jac_add(acc, p);
+  }
+  return acc;
+}
+
+// Jacobian q == affine (x, y) (not infinity)
+template <class F>
+__device__ __forceinline__ bool jac_eq_affine(const Jac<F>& q, const F& x, const F& y) {
+  if (jac_is_zero(q)) return false;
+  const F z2 = fsqr(q.z);
+  if (!fisz(fsub(q.x, fmul(x, z2)))) return false;
+  return fisz(fsub(q.y, fmul(y, fmul(z2, q.z))));
+}
+
+// [-x^2] P == phi(P)  <=>  [|x|]([|x|] P) == -phi(P) = (beta x, -y)
+__device__ __forceinline__ bool g1_in_subgroup(const Fp& x, const Fp& y) {
+  const Jac<Fp> q = mul_absx_jac(mul_absx_affine(x, y));
+  return jac_eq_affine(q, fp_mul(x, fp_const(BETA_M)), fp_neg(y));
+}
+
+// [x] P == psi(P)  <=>  [|x|] P == -psi(P);  psi(x) = conj(x) * (c1 u) = (x1 c1) + (x0 c1) u,
+// psi(y) = conj(y) * c2
+__device__ __forceinline__ bool g2_in_subgroup(const Fp2& x, const Fp2& y) {
+  const Jac<Fp2> q = mul_absx_affine(x, y);
+  const Fp c1 = fp_const(PSI_C1_C1);
+  const Fp2 px = {fp_mul(x.c1, c1), fp_mul(x.c0, c1)};
+  const Fp2 py = f2_mul(f2_conj(y), Fp2{fp_const(PSI_C2_C0), fp_const(PSI_C2_C1)});
+  return jac_eq_affine(q, px, f2_neg(py));
+}
+
+// ---------------------------------------------------------------------------- decompression
 __global__ void __launch_bounds__(256) k_g1_decompress(int n, const uint32_t* __restrict__ xw,
                                                        const uint8_t* __restrict__ flags, uint32_t* __restrict__ out,
                                                        uint8_t* __restrict__ ok) {
@@ -55,9 +104,7 @@ __global__ void __launch_bounds__(256) k_g1_decompress(int n, const uint32_t* __
     if (words_gt(p, x, 12)) {  // x < p
       const Fp xm = fp_from_words(x);
       const Fp rhs = fp_add(fp_mul(fp_sqr(xm), xm), fp_const(B1_M));
-      uint32_t e[12];
-      sqrt_exp_words(e);
-      Fp ym = fp_pow_words(rhs, e);
+      Fp ym = fp_mul(rhs, fp_pow_pm3d4(rhs));  // rhs^((p+1)/4)
       if (fp_eq(fp_sqr(ym), rhs)) {
         // "greatest" = y > p - y, i.e. y > (p - 1) / 2
         fp_to_words(ym, y);
@@ -68,10 +115,7 @@ __global__ void __launch_bounds__(256) k_g1_decompress(int n, const uint32_t* __
           ym = fp_neg(ym);
           fp_to_words(ym, y);
         }
-        // prime-order subgroup: r * P == O
-        uint32_t r[8];
-        for (int k = 0; k < 8; k++) r[k] = FR_W[k];
-        valid = jac_is_zero(jac_mul_affine(xm, ym, false, r));
+        valid = g1_in_subgroup(xm, ym);
       }
     }
   }
@@ -94,47 +138,30 @@ __device__ __forceinline__ bool f2_gt_canon(const Fp2& a, const Fp2& b) {
   return eq1 ? words_gt(a0, b0, 12) : words_gt(a1, b1, 12);
 }
 
-__device__ __forceinline__ Fp2 f2_pow_words(const Fp2& a, const uint32_t e[12]) {
-  Fp2 r = f2_one();
-  for (int i = 12 * 32 - 1; i >= 0; i--) {
-    r = f2_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1) r = f2_mul(r, a);
-  }
-  return r;
-}
-
-__device__ __forceinline__ bool f2_is_minus_one(const Fp2& a) {
-  return fp_eq(a.c0, fp_neg(fp_one())) && fp_is_zero(a.c1);
-}
-
-// square root in Fp2 for p = 3 mod 4 (Adj / Rodriguez-Henriquez): false when a is not a square
-__device__ __forceinline__ bool f2_sqrt(const Fp2& a, Fp2& out) {
-  if (f2_is_zero(a)) {
-    out = f2_zero();
-    return true;
-  }
-  uint32_t e[12];
-  for (int i = 0; i < 12; i++) e[i] = PM2_W[i];
-  e[0] -= 1;  // p - 3 (no borrow: the low word of p - 2 is 0xffffaaa9)
-  for (int i = 0; i < 12; i++) e[i] = (e[i] >> 2) | (i < 11 ? (e[i + 1] << 30) : 0u);  // (p - 3) / 4
-  const Fp2 a1 = f2_pow_words(a, e);
-  const Fp2 alpha = f2_mul(f2_sqr(a1), a);
-  const Fp2 a0 = f2_mul(f2_conj(alpha), alpha);  // alpha^p * alpha
-  if (f2_is_minus_one(a0)) return false;
-  const Fp2 x0 = f2_mul(a1, a);
-  Fp2 res;
-  if (f2_is_minus_one(alpha)) {
-    res = {fp_neg(x0.c1), x0.c0};  // x0 * u
-  } else {
-    uint32_t h[12];
-    for (int i = 0; i < 12; i++) h[i] = PM2_W[i];
-    h[0] += 1;  // p - 1
-    for (int i = 0; i < 12; i++) h[i] = (h[i] >> 1) | (i < 11 ? (h[i + 1] << 31) : 0u);  // (p - 1) / 2
-    res = f2_mul(f2_pow_words(f2_add(f2_one(), alpha), h), x0);
-  }
-  const Fp2 chk = f2_sub(f2_sqr(res), a);
-  out = res;
-  return f2_is_zero(chk);
+// Square root in Fp2 by the norm (two Fp exponentiations by (p-3)/4 instead of two Fp2 ones):
+// a = a0 + a1 u is a square iff N = a0^2 + a1^2 is a square in Fp; with s = sqrt(N) and
+// t = (a0 + s) / 2 (or (a0 - s) / 2 when that is 0), w = t^((p-3)/4):
+//   t w^2 ==  1 (t a square):      y = t w + (a1 w / 2) u
+//   t w^2 == -1 (-t a square; p = 3 mod 8 makes (-1)^((p-3)/4) = 1, so w serves -t too):
+//                                  y = a1 w / 2 - (t w) u
+// (t (a0 - s)/2 = -a1^2 / 4 is a non-square for a1 != 0, so exactly one case holds.)  Any root:
+// the caller picks the sign.  false when a is not a square.
+__device__ __forceinline__ bool f2_sqrt_norm(const Fp2& a, Fp2& out) {
+  out = f2_zero();
+  if (f2_is_zero(a)) return true;
+  const Fp nrm = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  const Fp s = fp_mul(nrm, fp_pow_pm3d4(nrm));
+  if (!fp_eq(fp_sqr(s), nrm)) return false;
+  const Fp half = fp_const(INV2_M);
+  Fp t = fp_mul(fp_add(a.c0, s), half);
+  if (fp_is_zero(t)) t = fp_mul(fp_sub(a.c0, s), half);
+  const Fp w = fp_pow_pm3d4(t);
+  const Fp tw = fp_mul(t, w);
+  const Fp aw = fp_mul(fp_mul(a.c1, half), w);
+  const bool qr = fp_eq(fp_mul(tw, w), fp_one());
+  const Fp2 y = qr ? Fp2{tw, aw} : Fp2{aw, fp_neg(tw)};
+  out = y;
+  return f2_is_zero(f2_sub(f2_sqr(y), a));
 }
 
 __global__ void __launch_bounds__(256) k_g2_decompress(int n, const uint32_t* __restrict__ xw,
@@ -159,14 +186,12 @@ __global__ void __launch_bounds__(256) k_g2_decompress(int n, const uint32_t* __
       const Fp2 b2 = {fp_const(B1_M), fp_const(B1_M)};  // 4 (1 + u)
       const Fp2 rhs = f2_add(f2_mul(f2_sqr(xm), xm), b2);
       Fp2 ym;
-      if (f2_sqrt(rhs, ym)) {
+      if (f2_sqrt_norm(rhs, ym)) {
         const Fp2 ny = f2_neg(ym);
         if (f2_gt_canon(ym, ny) != ((f & hbl::WIRE_GREATEST) != 0)) ym = ny;
         fp_to_words(ym.c0, y);
         fp_to_words(ym.c1, y + 12);
-        uint32_t r[8];
-        for (int k = 0; k < 8; k++) r[k] = FR_W[k];
-        valid = jac_is_zero(jac_mul_affine(xm, ym, false, r));
+        valid = g2_in_subgroup(xm, ym);
       }
     }
   }

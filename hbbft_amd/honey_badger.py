@@ -179,8 +179,13 @@ def _serialize(trace, corrupt=()):
     trace.raw_dec = dict(zip(dk, wire.encode_dec_share_msgs([trace.dec_shares[k] for k in dk])))
     ps = sorted(trace.cts)
     trace.raw_cts = dict(zip(ps, wire.encode_ciphertexts([trace.cts[p] for p in ps])))
+    if getattr(trace, "ba", None) is not None:  # BA coin shares, keyed (p, e, j)
+        bk = sorted(trace.ba.shares)
+        trace.raw_ba = dict(zip(bk, wire.encode_sig_share_msgs([trace.ba.shares[k] for k in bk])))
     for c in corrupt:
-        if c[0] == "ct":
+        if c[0] == "ba":
+            trace.raw_ba[c[1:]] = trace.raw_ba[c[1:]][:-1]              # truncated
+        elif c[0] == "ct":
             b = trace.raw_cts[c[1]]
             trace.raw_cts[c[1]] = b[:8] + bytes([b[8] ^ 0x01]) + b[9:]  # a compressed x that is not on the curve
         else:
@@ -594,7 +599,7 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
     t0 = time.perf_counter()
     if ba:
         coin_out = _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined, coin_prefetch,
-                             start_preverify)
+                             start_preverify, raw)
         coin_sh, dec_sh = ({}, {}) if raw else (trace.coin_shares, trace.dec_shares)
         handed = {}
         ni_sign = None
@@ -611,7 +616,7 @@ def _run_epoch(engine, keys, trace, window, our, threads, pipelined, slack, defe
 
 
 def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipelined=False, coin_prefetch=None,
-              after_first_drain=None):
+              after_first_drain=None, raw=False):
     """The BA-driven coin phase: one BinaryAgreementCoin per proposer with a coin (trace.ba).
     Messages (p, e, j) come in windows; before a window's drain, every share of a running or
     FUTURE epoch of its instance is queued (coin documents are hashed when first seen; a future
@@ -693,7 +698,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
     pks = keys.pks
 
     def queue_window(batch):
-        shares, qsig = ba.shares, ver._qsig  # (a drain replaces ver._qsig; none runs in here)
+        shares, qsig = bsh, ver._qsig  # (a drain replaces ver._qsig; none runs in here)
         for m in batch:
             p, e, j = m
             b = bas[p]
@@ -713,7 +718,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
                     queued_n[pe] = c + 1
 
     def hand_window(batch, end):
-        shares, fast = ba.shares, ver.shortcuts
+        shares, fast = bsh, ver.shortcuts
         t_msgs = time.perf_counter()
         for m in batch:
             p, e, j = m
@@ -729,7 +734,7 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
             if b.handle_fast(j, e, shares[m]):
                 continue
             try:
-                step = b.handle_message(j, e, ba.shares[m])
+                step = b.handle_message(j, e, shares[m])
             except ProtocolError as err:
                 res.errors.append(("coin", p, err))
                 continue
@@ -757,6 +762,17 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
     for w0 in range(0, len(msgs), window):
         batch = msgs[w0:w0 + window]
         t_q = time.perf_counter()
+        if raw:
+            pts = wire.decode_sig_share_msgs(engine, [trace.raw_ba[m] for m in batch])
+            good = []
+            for m, pt in zip(batch, pts):
+                if pt is None:
+                    res.faults.append(("coin", m[0], Fault(m[2], "DeserializeMessage")))
+                else:
+                    bsh[m] = pt
+                    good.append(m)
+            batch = good
+            res.timing["coin_decode"] = res.timing.get("coin_decode", 0.0) + time.perf_counter() - t_q
         queue_window(batch)
         res.timing["coin_queue"] = res.timing.get("coin_queue", 0.0) + time.perf_counter() - t_q
         if not pipelined:

@@ -125,3 +125,23 @@ def bivar_row_fd(t, ymin, ymax, nacks, val_windows=16):
     steps = _scale(G1_ADD, t * (ymax - y0))
     acks = _scale(_add(_scale(G1_MADD, val_windows), (4, 2)), nacks)
     return _add(*parts, steps, acks)
+
+
+# ---------------------------------------------------------------------------- wire decoding (round 6)
+# k_g1_decompress / k_g2_decompress per valid point (csrc/k_wire.hip).  The square root's one
+# exponent (p-3)/4 is tools/gen_sqrt_chain.py's width-4 sliding-window chain: a^2 + 375 squarings
+# and 7 table + 78 window products.
+SQRT_CHAIN = (376 + 85, 376)
+G2_DBL = (2 * F2M + 5 * F2S, 0)          # dbl-2009-l over Fp2 (Fp2 squarings are Fp products)
+G2_MADD = (7 * F2M + 4 * F2S, 0)         # madd-2007-bl over Fp2
+# G1: to Montgomery, x^3 + 4, y = rhs * rhs^((p-3)/4) and its check, canonical y; subgroup by
+# phi(P) == [-x^2] P: [|x|] twice (63 doublings + 5 mixed / 5 general additions), beta x and the
+# Jacobian-affine compare
+WIRE_G1_DECODE = _add((1, 0), (2, 1), SQRT_CHAIN, (2, 1), (1, 0),
+                      _scale(G1_DBL, 2 * NBITS), _scale(G1_MADD, NADD), _scale(G1_ADD, NADD), (5, 1))
+# G2: to Montgomery, x^3 + b, the norm-method root (norm, two chains, s, t, t w, a1 w / 2, t w^2,
+# the y^2 check), the sign's canonical compare; subgroup by psi(P) == [x] P: [|x|] (63 doublings +
+# 5 mixed additions), psi and the compare
+WIRE_G2_DECODE = _add((2, 0), (F2S + F2M, 0), (2, 2), _scale(SQRT_CHAIN, 2), (1, 0), (1, 1), (1, 0),
+                      (1, 0), (2, 0), (1, 0), (F2S, 0), (6, 0),
+                      _scale(G2_DBL, NBITS), _scale(G2_MADD, NADD), (2 + F2M, 0), (F2S + 3 * F2M, 0))

@@ -535,8 +535,10 @@ class DecodeError(ValueError):
     pass
 
 
-def g1_decompress(b):
-    """pairing 0.14 ``G1Compressed::into_affine``: flags, on-curve and subgroup checks."""
+def g1_decompress(b, in_subgroup=None):
+    """pairing 0.14 ``G1Compressed::into_affine``: flags, on-curve and subgroup checks.
+    ``in_subgroup``: the r * P == O test to use (default the pure-Python one; tests pass the C
+    oracle's scalar multiplication for large samples)."""
     if len(b) != 48:
         raise DecodeError("length")
     if not (b[0] & 0x80):
@@ -556,12 +558,12 @@ def g1_decompress(b):
     if (y > ny) != greatest:
         y = ny
     pt = (x, y)
-    if not g1_in_subgroup(pt):
+    if not (in_subgroup or g1_in_subgroup)(pt):
         raise DecodeError("not in subgroup")
     return pt
 
 
-def g2_decompress(b):
+def g2_decompress(b, in_subgroup=None):
     if len(b) != 96:
         raise DecodeError("length")
     if not (b[0] & 0x80):
@@ -583,7 +585,7 @@ def g2_decompress(b):
     if f2_gt(y, ny) != greatest:
         y = ny
     pt = (x, y)
-    if not g2_in_subgroup(pt):
+    if not (in_subgroup or g2_in_subgroup)(pt):
         raise DecodeError("not in subgroup")
     return pt
 

@@ -103,3 +103,27 @@ def test_sync_key_gen_from_raw_bytes(engine):
         assert [o.fault for o in r1] == [o.fault for o in r2] and all(o.valid for o in r1)
     for kg, tw in zip(nodes, twins):
         assert kg.generate() == tw.generate()
+
+
+def test_ba_epoch_from_raw_bytes(engine):
+    """BA-driven coins fed bincode coin-share messages (round 6: the raw epoch line): each window
+    is decoded in one engine call before it is queued; outputs equal the point-fed epoch's, and a
+    truncated coin-share message is a DeserializeMessage fault of its sender that changes no
+    decision or coin."""
+    n, t = 7, 2
+    rng = random.Random(902)
+    keys = NetworkKeys(engine, n, t, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=5, bad_every=9, proposal_bytes=70)
+    trace.with_ba(engine, rng, extra=0.3, bad_every=11)
+    ref = run_epoch(engine, keys, trace, window=16)
+    trace.serialize()
+    raw = run_epoch(engine, keys, trace, window=16, raw=True)
+    assert (raw.plaintexts, raw.coins, raw.signatures) == (ref.plaintexts, ref.coins, ref.signatures)
+    assert (raw.ba_decisions, raw.ba_coins) == (ref.ba_decisions, ref.ba_coins)
+    key = lambda r: sorted((k, p, f.node_id, f.kind) for k, p, f in r.faults)
+    assert key(raw) == key(ref)
+    m = next(k for k in trace.ba.msgs if ("coin", k[0], k[2]) not in (trace.bad | trace.ba.bad) and k[2] != 0)
+    trace.serialize(corrupt=[("ba",) + tuple(m)])
+    bad = run_epoch(engine, keys, trace, window=16, raw=True)
+    assert ("coin", m[0], m[2], "DeserializeMessage") in {(k, p, f.node_id, f.kind) for k, p, f in bad.faults}
+    assert (bad.ba_decisions, bad.ba_coins, bad.plaintexts) == (ref.ba_decisions, ref.ba_coins, ref.plaintexts)
