@@ -624,8 +624,12 @@ def _ba_coins(engine, keys, trace, ver, window, our, threads, limit, res, pipeli
     SBV / Conf outcomes whose release position has passed are fired, and the window's coin combines
     run as one deferred batch whose results resume the BA state machines (which may replay queued
     shares and complete further coins: repeated until no combine is pending).  Returns
-    {p: signature of the instance's first threshold coin}, as the synthetic phase does."""
+    {p: signature of the instance's first threshold coin}, as the synthetic phase does.
+    ``raw``: the coin-share messages arrive as bincode bytes (trace.raw_ba); each window is decoded
+    in one batched engine call before it is queued, and a message that does not decode is dropped
+    as a ``DeserializeMessage`` fault of its sender (as _windows does)."""
     ba = trace.ba
+    bsh = {} if raw else ba.shares  # the coin shares the flows read (decoded per window when raw)
     sk = keys.sks[our]
     hb_id = 0
     own_sig = {}

@@ -6,6 +6,7 @@ plus a subgroup point), the cofactor parts [r] Q, and subgroup points.  Accept /
 decoded bytes must be identical; the same through the _dev entry points."""
 import numpy as np
 import pytest
+import torch
 
 from oracle import bls12_381 as C
 from oracle import cbls
@@ -58,15 +59,14 @@ def test_decode_subgroup_matches_r_mul(engine, g2):
 @pytest.mark.parametrize("g2", [False, True], ids=["G1", "G2"])
 def test_decode_subgroup_dev_entry(engine, g2):
     """The device-resident entry point (encodings already in HBM) gives the same verdicts."""
-    import torch
     sample = S.sample(g2, 64, seed=710 + g2)
     comp = C.g2_compress if g2 else C.g1_compress
     encs = [comp(pt) for _, pt in sample]
     want_pts, want_ok = oracle_decode(g2, encs)
     size, n = (96, 192) if g2 else (48, 96)
-    d_in = torch.from_numpy(np.frombuffer(b"".join(encs), dtype=np.uint8).copy()).cuda()
-    d_out = torch.zeros(len(encs) * n, dtype=torch.uint8, device="cuda")
-    d_ok = torch.zeros(len(encs), dtype=torch.uint8, device="cuda")
+    d_in = torch.from_numpy(np.frombuffer(b"".join(encs), dtype=np.uint8).copy()).to("cuda:0")
+    d_out = torch.zeros(len(encs) * n, dtype=torch.uint8, device="cuda:0")
+    d_ok = torch.zeros(len(encs), dtype=torch.uint8, device="cuda:0")
     (engine.g2_decompress_dev if g2 else engine.g1_decompress_dev)(None, len(encs), d_in.data_ptr(), d_out.data_ptr(),
                                                                    d_ok.data_ptr())
     torch.cuda.synchronize()
