@@ -499,6 +499,9 @@ class BinaryAgreement:
         step = Step(fault_log=[Fault(f.node_id, "CoinFault:" + f.kind) for f in ts_step.fault_log],
                     messages=[(t, (epoch, ("Coin", s))) for t, s in ts_step.messages])
         if ts_step.output:
+            if isinstance(ts_step.output[0], Deferred):  #  BinaryAgreementCoin resolves these
+                raise ProtocolError("BinaryAgreement needs a non-recording verifier: its coin's combined "
+                                    "signature is deferred (use BinaryAgreementCoin with resolve_pending)")
             self.coin_value, self.ts = signature_parity(ts_step.output[0]), None
             self.coins[epoch] = self.coin_value
             step.extend(self._try_update_epoch())

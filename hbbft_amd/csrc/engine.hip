@@ -1848,11 +1848,19 @@ int hbh_bivar_ack_check_set(hbh_commit_set* cs, size_t nack, const uint32_t* par
   HBH_CHECK(hipMemcpyAsync(e->in_c.p, vals, nack * HBH_FR_BYTES, hipMemcpyHostToDevice, s));
   rc = ensure_fbtab(e, s);
   if (rc) return rc;
+  if (!fd.slot.empty() && ensure_fb16(e, s) != HBH_OK) {
+    // the 16-bit comb (96 MiB + ~192 MiB of build scratch) could not be built: the Horner kernel
+    // checks every ack (same verdicts), and this engine stops planning FD runs
+    e->fb16.release();
+    e->ack_fd = false;
+    static std::once_flag warned;
+    std::call_once(warned, [] { fprintf(stderr, "hbbft_hip: no memory for the FD ack comb; Horner ack checks\n"); });
+    fd = FdPlan();
+    order_by_y(nack, ys, order);
+  }
   const size_t nfd = fd.slot.size();
   uint32_t* d_fd = nullptr;
   if (nfd) {
-    rc = ensure_fb16(e, s);
-    if (rc) return rc;
     const size_t words = 4 * nfd + 2 * nack;
     HBH_CHECK(e->fd_meta.ensure(words * 4));
     HBH_CHECK(e->fd_e.ensure(fd.npts * hbl::fd_point_bytes()));

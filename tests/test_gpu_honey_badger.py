@@ -280,3 +280,21 @@ def test_ba_epoch_pipelined_and_prefetch_equal_serial(engine, n):
         assert _outcome(pip) == _outcome(serial)
         assert _outcome(pre) == _outcome(serial)
         assert _outcome(full) == _outcome(serial)
+
+
+@pytest.mark.parametrize("adversary", ["random", "faulty_share"])
+def test_speculative_g1_combines_equal_off(engine, monkeypatch, adversary):
+    """the speculative decryption combines of the pre-verification (HBH_EPOCH_SPEC_G1,
+    on by default) change no outcome -- the same decisions, coins, signatures, plaintexts, faults in
+    order and errors with them off, under an adversary forging decryption and coin shares."""
+    rng = random.Random({"random": 5200, "faulty_share": 5201}[adversary])
+    keys = NetworkKeys(engine, 16, 5, rng)
+    trace = EpochTrace.generate(engine, keys, rng, hb_epoch=2, bad_every=7, proposal_bytes=90, n_adv=5,
+                                adversary=adversary, inject=0.3)
+    trace.with_ba(engine, rng, extra=0.3, bad_every=9)
+    monkeypatch.setenv("HBH_EPOCH_SPEC_G1", "1")
+    on = run_epoch(engine, keys, trace, window=64)
+    monkeypatch.setenv("HBH_EPOCH_SPEC_G1", "0")
+    off = run_epoch(engine, keys, trace, window=64)
+    assert _outcome(on) == _outcome(off)
+    assert on.plaintexts == trace.proposals and on.errors == []
