@@ -86,7 +86,7 @@ SIGNATURES = [
     ("hbh_hash_bp_g1", _I, [_P]),
 ]
 STAGE_PREPARE, STAGE_PAIRING, STAGE_CURVE = 0, 1, 2
-IMPL_AUTO, IMPL_PAIR, IMPL_WAVE, IMPL_QUAD, IMPL_OCT = 3, 4, 5, 6, 7   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)
+IMPL_AUTO, IMPL_PAIR, IMPL_WAVE, IMPL_QUAD, IMPL_OCT, IMPL_WAVE2 = 3, 4, 5, 6, 7, 8   # HBH_IMPL_* (0, 1, 2 = retired THREAD, LANE_COOP, THREAD_SIGNED)
 ACK_AUTO, ACK_QUAD, ACK_LANE, ACK_LANE_HORNER = 0, 1, 2, 3  # HBH_ACK_*
 
 _lib = None

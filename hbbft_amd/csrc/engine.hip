@@ -167,6 +167,7 @@ int end_call(hbh_engine* e, hipStream_t s) {
 
 int resolve_impl(const hbh_engine* e, size_t n) {
   if (e->impl != HBH_IMPL_AUTO) return e->impl;
+  if (n <= HBH_AUTO_WAVE2_MAX) return HBH_IMPL_WAVE2;
   if (n <= HBH_AUTO_WAVE_MAX) return HBH_IMPL_WAVE;
   if (n <= HBH_AUTO_OCT_MAX) return HBH_IMPL_OCT;
   return n <= HBH_AUTO_QUAD_MAX ? HBH_IMPL_QUAD : HBH_IMPL_PAIR;
@@ -186,6 +187,14 @@ hbl::PairSideDesc offset_side(const hbl::PairSideDesc& d, size_t off) {
   return o;
 }
 
+// HBH_IMPL_WAVE2 (two waves per check) takes plain checks only; the split master check's modes
+// (Miller-only, Jacobian P, one side) run on WAVE
+hipError_t wave2_verify(hipStream_t s, int n, const hbl::PairSideDesc& a, const hbl::PairSideDesc& b, int flags,
+                        uint8_t* v, uint32_t* val) {
+  if (flags & ~(hbl::WAVE_NEG_P2 | hbl::WAVE_CONJ_VALUE)) return hbl::wave_verify(s, n, a, b, flags, v, val);
+  return hbl::wave64_verify(s, n, a, b, flags, v, val);
+}
+
 // HBH_IMPL_AUTO's launches for n checks on one stream (profiles/r04/c8, c19, c20 sweeps): whole
 // rounds of HBH_AUTO_PAIR_ROUND checks (two lane-pair waves per SIMD) on PAIR, then the remainder by
 // size -- above HBH_AUTO_SPLIT_HI one more (partial) PAIR round; above HBH_AUTO_SPLIT_LO PAIR on
@@ -201,6 +210,7 @@ hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, con
     const hbl::PairSideDesc a = o ? offset_side(s1, o) : s1, b = o ? offset_side(s2, o) : s2;
     uint8_t* v = d_v ? d_v + o : nullptr;
     uint32_t* val = d_value ? d_value + o * 144 : nullptr;
+    if (kind == HBH_IMPL_WAVE2) return wave2_verify(s, (int)cnt, a, b, flags, v, val);
     if (kind == HBH_IMPL_WAVE) return hbl::wave_verify(s, (int)cnt, a, b, flags, v, val);
     if (kind == HBH_IMPL_QUAD) return hbl::quad_verify(s, (int)cnt, a, b, flags, v, val);
     if (kind == HBH_IMPL_OCT) return hbl::oct_verify(s, (int)cnt, a, b, flags, v, val);
@@ -222,6 +232,7 @@ hipError_t verify_auto(hipStream_t s, size_t n, const hbl::PairSideDesc& s1, con
     off += HBH_AUTO_SPLIT_LO;
     rem -= HBH_AUTO_SPLIT_LO;
   }
+  if (rem <= HBH_AUTO_WAVE2_MAX) return at(off, rem, HBH_IMPL_WAVE2);
   if (rem <= HBH_AUTO_WAVE_MAX) return at(off, rem, HBH_IMPL_WAVE);
   if (rem <= HBH_AUTO_OCT_MAX) return at(off, rem, HBH_IMPL_OCT);
   if (rem <= HBH_AUTO_QUAD_MAX) return at(off, rem, HBH_IMPL_QUAD);
@@ -238,7 +249,7 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
   DevBuf* inf[2] = {&e->pinf[slot][0], &e->pinf[slot][1]};
   for (int k = 0; k < 2; k++) {
     // WAVE walks every side: a table costs a serial 68-step walk (k_oct_prep) before the first check
-    if (!sd[k].idx || sd[k].nq * 4 > n || impl == HBH_IMPL_WAVE) continue;
+    if (!sd[k].idx || sd[k].nq * 4 > n || impl == HBH_IMPL_WAVE || impl == HBH_IMPL_WAVE2) continue;
     HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
     HBH_CHECK(inf[k]->ensure(sd[k].nq));
     hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);
@@ -252,6 +263,8 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
     HBH_CHECK(verify_auto(s, n, sd[0], sd[1], flags, d_v, d_value));
   else if (impl == HBH_IMPL_WAVE)
     HBH_CHECK(hbl::wave_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
+  else if (impl == HBH_IMPL_WAVE2)
+    HBH_CHECK(wave2_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   else if (impl == HBH_IMPL_QUAD)
     HBH_CHECK(hbl::quad_verify(s, (int)n, sd[0], sd[1], flags, d_v, d_value));
   else if (impl == HBH_IMPL_OCT)
@@ -505,7 +518,7 @@ int hbh_dbg_pairing(hbh_engine* e, size_t n, const uint8_t* p, const uint8_t* q,
 int hbh_engine_set_pairing_impl(hbh_engine* e, int impl) {
   if (!e) return fail(HBH_ERR_ARG, "null engine");
   if (impl != HBH_IMPL_PAIR && impl != HBH_IMPL_AUTO && impl != HBH_IMPL_WAVE && impl != HBH_IMPL_QUAD &&
-      impl != HBH_IMPL_OCT)
+      impl != HBH_IMPL_OCT && impl != HBH_IMPL_WAVE2)
     return fail(HBH_ERR_ARG, "unknown or retired pairing implementation");
   std::lock_guard<std::mutex> lk(e->mu);
   e->impl = impl;

@@ -72,6 +72,14 @@ hipError_t wave_prod_fe(hipStream_t s, int n, int nf, const uint32_t* fin, uint8
 size_t wave_tree_counter_bytes(int ngroup, int nw);
 hipError_t wave_miller_tree(hipStream_t s, int ngroup, int nw, const PairSideDesc& s1, const PairSideDesc& s2,
                             int flags, uint32_t* value_out, uint32_t* counters, uint8_t* verdict);
+// The same verdicts / values as wave_verify with TWO waves (64 lane pairs) per check (k_wave64.hip,
+// round 6): 149 Miller stages per two-pair check instead of 210-211 -- the latency kernel for calls
+// of few checks.  Plain checks only (flags WAVE_NEG_P2 / WAVE_CONJ_VALUE).
+constexpr int WAVE_NEG_P2 = 1;
+constexpr int WAVE_CONJ_VALUE = 2;
+size_t wave64_lds_bytes();
+hipError_t wave64_verify(hipStream_t s, int n, const PairSideDesc& s1, const PairSideDesc& s2, int flags,
+                         uint8_t* verdict, uint32_t* value_out);
 
 // --------------------------------------------------------------- curve / MSM (k_curve.hip)
 // out[i] = k_i * P_i (G1 or G2 ABI words; scalars 8 LE words, any 256-bit integer).

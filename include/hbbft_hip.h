@@ -322,7 +322,12 @@ int hbh_fr_poly_eval(size_t npoly, size_t ncoef, const uint8_t* coeffs, size_t n
  *     ~0.55 of its per-lane time).  Mid-size path: 16,384 checks are one wave per SIMD.
  *   HBH_IMPL_OCT (k_oct.hpp): EIGHT lanes per check -- four lane pairs, four independent products per
  *     round.  Small-batch path: 8,192 checks are one wave per SIMD.
- *   HBH_IMPL_AUTO (the default): WAVE up to HBH_AUTO_WAVE_MAX checks per call, OCT up to
+ *   HBH_IMPL_WAVE2 (k_wave64.hip, round 6): TWO 64-lane waves per check (64 lane pairs): the Miller
+ *     loop multiplies a step's two lines together beside f^2 and takes their product in one stage,
+ *     149 stages per two-pair check instead of WAVE's 210-211.  Latency path for calls of up to
+ *     HBH_AUTO_WAVE2_MAX checks (AUTO; plain checks -- the split master check's modes stay on WAVE).
+ *   HBH_IMPL_AUTO (the default): WAVE2 up to HBH_AUTO_WAVE2_MAX checks per call, WAVE up to
+ *     HBH_AUTO_WAVE_MAX checks per call, OCT up to
  *     HBH_AUTO_OCT_MAX, QUAD up to HBH_AUTO_QUAD_MAX (each one wave per SIMD at its maximum), PAIR
  *     above -- the measured crossovers (profiles/r04/c8_sweep_wave_quad_pair.txt,
  *     c23_oct_wave_sweep.txt, kernel ms per call on the sign workload): 4,096 checks WAVE 5.3 /
@@ -344,6 +349,8 @@ int hbh_fr_poly_eval(size_t npoly, size_t ncoef, const uint8_t* coeffs, size_t n
 #define HBH_IMPL_WAVE 5
 #define HBH_IMPL_QUAD 6
 #define HBH_IMPL_OCT 7
+#define HBH_IMPL_WAVE2 8
+#define HBH_AUTO_WAVE2_MAX 256  /* AUTO: WAVE2 up to here (two waves per check), then WAVE */
 #define HBH_AUTO_WAVE_MAX 4096
 #define HBH_AUTO_OCT_MAX 8192
 #define HBH_AUTO_QUAD_MAX 16384

@@ -141,7 +141,7 @@ def _sign_batch(engine, rng, ndocs, per_doc):
     return ([pks[i % per_doc] for i in range(n)], sigs, hs, [i // per_doc for i in range(n)], want)
 
 
-@pytest.mark.parametrize("impl", [4, 5], ids=["pair", "wave"])
+@pytest.mark.parametrize("impl", [4, 5, 8], ids=["pair", "wave", "wave2"])
 def test_dev_calls_on_two_streams(engine, impl):
     """Two hbh_verify_pairing_eq_dev calls queued back-to-back on two different streams:
     the second call's line tables must not overwrite the first call's while its kernels still read
@@ -169,9 +169,9 @@ def test_dev_calls_on_two_streams(engine, impl):
         engine.set_pairing_impl(IMPL_AUTO)
 
 
-@pytest.mark.parametrize("impl", [4, 5, 6, 7], ids=["pair", "wave", "quad", "oct"])
+@pytest.mark.parametrize("impl", [4, 5, 6, 7, 8], ids=["pair", "wave", "quad", "oct", "wave2"])
 def test_dev_index_out_of_range_rejects(engine, impl):
-    """HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD and HBH_IMPL_OCT validate device index arrays in-kernel: an index >= its table
+    """HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD, HBH_IMPL_OCT and HBH_IMPL_WAVE2 validate device index arrays in-kernel: an index >= its table
     size gives verdict 0 for that item only (never a read past the table)."""
     from hbbft_amd._lib import IMPL_AUTO
     rng = random.Random(9)

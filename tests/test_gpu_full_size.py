@@ -17,7 +17,7 @@ import pytest
 
 from oracle import bls12_381 as C
 from oracle import cbls, tc
-from hbbft_amd._lib import IMPL_AUTO, IMPL_OCT, IMPL_QUAD, IMPL_WAVE
+from hbbft_amd._lib import IMPL_AUTO, IMPL_OCT, IMPL_QUAD, IMPL_WAVE, IMPL_WAVE2
 from hbbft_amd.engine import g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a
 
 pytestmark = pytest.mark.gpu
@@ -54,7 +54,8 @@ def sign_batch(engine):
     return dict(coeffs=coeffs, sks=sks, pks=pks, mpk=mpk, hashes=hashes, sigs=sigs, expected=expected)
 
 
-@pytest.mark.parametrize("impl", [IMPL_AUTO, IMPL_WAVE, IMPL_QUAD, IMPL_OCT], ids=["auto", "wave", "quad", "oct"])
+@pytest.mark.parametrize("impl", [IMPL_AUTO, IMPL_WAVE, IMPL_QUAD, IMPL_OCT, IMPL_WAVE2],
+                         ids=["auto", "wave", "quad", "oct", "wave2"])
 def test_config1_65536_sig_shares(engine, sign_batch, impl):
     b = sign_batch
     n = NDOCS * N
@@ -71,9 +72,9 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
         assert cbls.verify_g2(b["pks"][i % N], b["sigs"][i], b["hashes"][i // N]) == bool(v[i]), i
 
 
-@pytest.mark.parametrize("n", [4096, 4160, 8192, 8256, 16384, 16448, 32768, 32832, 49152, 49216],
-                         ids=["wave_max", "oct_min", "oct_max", "quad_min", "quad_max", "pair_min", "split_lo",
-                              "split_min", "split_max", "pair2_min"])
+@pytest.mark.parametrize("n", [256, 320, 4096, 4160, 8192, 8256, 16384, 16448, 32768, 32832, 49152, 49216],
+                         ids=["wave2_max", "wave_min", "wave_max", "oct_min", "oct_max", "quad_min", "quad_max",
+                              "pair_min", "split_lo", "split_min", "split_max", "pair2_min"])
 def test_config1_at_auto_thresholds(engine, sign_batch, n):
     """Every kernel on both sides of the AUTO boundaries (HBH_AUTO_WAVE_MAX = 4,096 checks, 64
     documents of configs[1]; HBH_AUTO_OCT_MAX = 8,192, 128 documents; HBH_AUTO_QUAD_MAX = 16,384, 256
@@ -81,7 +82,7 @@ def test_config1_at_auto_thresholds(engine, sign_batch, n):
     G2 sides, OCT, QUAD and PAIR read H's line table; verdicts equal the construction."""
     b = sign_batch
     from hbbft_amd._lib import IMPL_PAIR, IMPL_QUAD
-    for impl in (IMPL_WAVE, IMPL_OCT, IMPL_QUAD, IMPL_PAIR, IMPL_AUTO):
+    for impl in (IMPL_WAVE2, IMPL_WAVE, IMPL_OCT, IMPL_QUAD, IMPL_PAIR, IMPL_AUTO):
         engine.set_pairing_impl(impl)
         try:
             v = engine.verify_sig_shares([b["pks"][i % N] for i in range(n)], b["sigs"][:n], b["hashes"][:n // N],

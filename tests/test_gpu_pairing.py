@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.fixture(params=[4, 5, 6, 7, 3], ids=["pair", "wave", "quad", "oct", "auto"])
+@pytest.fixture(params=[4, 5, 6, 7, 8, 3], ids=["pair", "wave", "quad", "oct", "wave2", "auto"])
 def eng(engine, request):
-    """Every pairing implementation (HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD, HBH_IMPL_OCT) and the default
-    HBH_IMPL_AUTO must give identical results."""
+    """Every pairing implementation (HBH_IMPL_PAIR, HBH_IMPL_WAVE, HBH_IMPL_QUAD, HBH_IMPL_OCT,
+    HBH_IMPL_WAVE2) and the default HBH_IMPL_AUTO must give identical results."""
     engine.set_pairing_impl(request.param)
     yield engine
     engine.set_pairing_impl(3)
@@ -125,10 +125,13 @@ def test_implementations_agree_random_batch(engine):
         v5 = engine.verify_sig_shares(P, S, hs, D)
         engine.set_pairing_impl(6)
         v6 = engine.verify_sig_shares(P, S, hs, D)
+        engine.set_pairing_impl(8)
+        v8 = engine.verify_sig_shares(P, S, hs, D)
     finally:
         engine.set_pairing_impl(3)
     assert v5 == v0
     assert v6 == v0
+    assert v8 == v0
     for i, w in want:
         assert v0[i] == int(w), i
     assert sum(v0) == sum(1 for i in range(n) if i % 11 not in (3, 5))

@@ -167,3 +167,60 @@ def test_single_pair_homogeneous_walk(progs):
         fs = [W.emulate_miller(v1, [(jac(Pp), Q, False)]),
               W.emulate_miller(v1, [(jac((m[0], (-m[1]) % C.P)), C.G2_GEN, False)])]
         assert (W.emulate_prod_fe(v, fs) == ONE_W) == want1
+
+
+# ---------------------------------------------------------------- the 64-pair set (k_wave64, round 6)
+@pytest.fixture(scope="module")
+def progs64():
+    return W.build(64)
+
+
+def test_committed_include64_is_current(progs64, tmp_path):
+    p = tmp_path / "wave_prog64.inc"
+    W.emit(progs64, str(p), ns="hbw64")
+    with open(os.path.join(ROOT, "hbbft_amd", "csrc", "wave_prog64.inc")) as f:
+        assert f.read() == p.read_text(), "regenerate with python tools/gen_wave_prog.py"
+
+
+def test_program_shape64(progs, progs64):
+    """Combined lines (op_mul_ll beside f^2, one op_mul_fl per step) and the homogeneous walk: two
+    stages per step where the 32-pair walking programs take three."""
+    for m, v in progs64["variants"].items():
+        assert v["nstages_miller"] <= 150 and v["nstages_fe"] == progs["variants"][m]["nstages_fe"], m
+        assert max(st.npairs for st in v["stages_miller"]) <= 64
+    assert progs["variants"]["TT"]["nstages_miller"] <= 140  # the 32-pair TT takes the combined lines too
+    assert progs64["nslots"] <= 170
+
+
+@pytest.mark.parametrize("mode", W.MODES64)
+def test_single_pairing_value64(progs64, mode):
+    rnd = random.Random(17 + W.MODES64.index(mode))
+    Pp = C.g1_mul(C.G1_GEN, rnd.randrange(1, C.R))
+    Q = C.g2_mul(C.G2_GEN, rnd.randrange(1, C.R))
+    got = W.emulate(progs64["variants"][mode], [(Pp, Q, False), (None, Q, False)], conj=True)
+    assert got == tower_to_w(cube(C.pairing(Pp, Q)))
+
+
+@pytest.mark.parametrize("mode", W.MODES64)
+def test_pairing_equality64(progs64, mode):
+    rnd = random.Random(21 + W.MODES64.index(mode))
+    a, b = rnd.randrange(1, C.R), rnd.randrange(1, C.R)
+    P1, Q1 = C.g1_mul(C.G1_GEN, a), C.g2_mul(C.G2_GEN, b)
+    Q2 = C.g2_mul(C.G2_GEN, a * b % C.R)
+    v = progs64["variants"][mode]
+    assert W.emulate(v, [(P1, Q1, False), ("GEN", Q2, True)]) == ONE_W
+    Q2bad = C.g2_mul(C.G2_GEN, (a * b + 1) % C.R)
+    assert W.emulate(v, [(P1, Q1, False), ("GEN", Q2bad, True)]) != ONE_W
+
+
+@pytest.mark.parametrize("mode", ["WT", "TW"])
+def test_inactive_pairs64(progs64, mode):
+    rnd = random.Random(23)
+    Pp = C.g1_mul(C.G1_GEN, rnd.randrange(1, C.R))
+    Q = C.g2_mul(C.G2_GEN, rnd.randrange(1, C.R))
+    v = progs64["variants"][mode]
+    assert W.emulate(v, [(None, Q, False), (Pp, None, False)]) == ONE_W
+    got = W.emulate(v, [(None, Q, False), (Pp, Q, False)], conj=True)
+    assert got == tower_to_w(cube(C.pairing(Pp, Q)))
+    got = W.emulate(v, [(Pp, Q, False), (None, Q, False)], conj=True)
+    assert got == tower_to_w(cube(C.pairing(Pp, Q)))

@@ -135,9 +135,20 @@ def op_sqr12(dst, src, conj_src=False):
     return Op("M1", prods, outs, name="sqr12")
 
 
-def op_mul12(dst, a, b, nega_odd=False, negb_odd=False, conj_out=False):
+def op_mul12(dst, a, b, nega_odd=False, negb_odd=False, conj_out=False, m1=False):
     """dst = a * b (with a / b conjugated in Fp12 when nega_odd / negb_odd, dst conjugated when
-    conj_out): 36 products, two per lane pair (M2)."""
+    conj_out): 36 products, two per lane pair (M2) -- or one per lane pair (M1) in the 64-pair
+    programs, where the 36 fit one stage."""
+    if m1:
+        prods, terms = [], {k: ([], []) for k in range(6)}
+        for i in range(6):
+            for j in range(6):
+                sgn = (-1 if (nega_odd and i % 2) else 1) * (-1 if (negb_odd and j % 2) else 1)
+                k = (i + j) % 6
+                c = sgn * (-1 if (conj_out and k % 2) else 1)
+                terms[k][1 if i + j >= 6 else 0].append((P_(len(prods)), c, 0))
+                prods.append([Prod(a[i], b[j])])
+        return Op("M1", prods, [Out(dst[k], *terms[k]) for k in range(6)], name="mul12m1")
     groups = {}
     for i in range(6):
         for j in range(6):
@@ -178,6 +189,37 @@ def op_mul_fp6(dst, f, t):
             terms[o % 6][1 if o >= 6 else 0].append((P_(len(prods)), 1, 0))
             prods.append([Prod(f[k], t[j])])
     return Op("M1", prods, [Out(dst[k], *terms[k]) for k in range(6)], name="mulfp6")
+
+
+def op_mul_ll(dst, a, b):
+    """dst = a * b for two 014-sparse lines (positions 0, 2, 3 of the w-basis): 9 products; the
+    result lives at positions 0, 2, 3, 4, 5 (w^6 = xi folds a3 b3 into position 0).  dst: 9 slots --
+    the five positions and xi times positions 2, 3, 4, 5, so that op_mul_fl's wrapped terms are plain
+    terms (an output of mixed plain / twisted terms would need 9 assembly terms per stage)."""
+    prods = [[Prod(a[0], b[0])], [Prod(a[2], b[2])], [Prod(a[0], b[1])], [Prod(a[1], b[0])], [Prod(a[0], b[2])],
+             [Prod(a[2], b[0])], [Prod(a[1], b[1])], [Prod(a[1], b[2])], [Prod(a[2], b[1])]]
+    pos = {0: [P_(0)], 2: [P_(2), P_(3)], 3: [P_(4), P_(5)], 4: [P_(6)], 5: [P_(7), P_(8)]}
+    outs = [Out(dst[0], [(P_(0), 1, 0)], [(P_(1), 1, 0)])]
+    for k, sh in enumerate(LL_POS[1:]):
+        outs.append(Out(dst[1 + k], [(q, 1, 0) for q in pos[sh]]))
+        outs.append(Out(dst[5 + k], [], [(q, 1, 0) for q in pos[sh]]))
+    return Op("M1", prods, outs, name="mulll")
+
+
+LL_POS = (0, 2, 3, 4, 5)
+
+
+def op_mul_fl(dst, f, ll):
+    """dst = f * ll, ll a product of two lines (op_mul_ll's 9 slots: positions 0, 2, 3, 4, 5, then
+    xi times positions 2, 3, 4, 5): 30 products, five plain terms per output."""
+    prods, terms = [], {k: [] for k in range(6)}
+    for k in range(6):
+        for q, sh in enumerate(LL_POS):
+            o = k + sh
+            slot = ll[q] if o < 6 else ll[4 + q]
+            terms[o % 6].append((P_(len(prods)), 1, 0))
+            prods.append([Prod(f[k], slot)])
+    return Op("M1", prods, [Out(dst[k], terms[k]) for k in range(6)], name="mulfl")
 
 
 def op_cyclo(dst, f, conj_out=False):
@@ -233,8 +275,9 @@ def op_copy(dst, src, conj_out=False):
 
 # ------------------------------------------------------------------------------- programs
 class Builder:
-    def __init__(self, name, cyc_runs=True):
+    def __init__(self, name, cyc_runs=True, m1=False):
         self.name = name
+        self.m1 = m1  # 64-pair programs: Fp12 products as 36 one-product pairs (M1) instead of 18 M2
         self.cyc_runs = cyc_runs  # final exponentiation squarings as CYC runs (False: one SQ stage each)
         self.slots = {}
         for c in CONSTS:
@@ -253,6 +296,9 @@ class Builder:
         if name not in self.slots:
             self.slots[name] = len(self.slots)
         return self.slots[name]
+
+    def mul12(self, *a, **k):
+        return op_mul12(*a, m1=self.m1, **k)
 
     def group(self, name, n=6):
         return [name + str(k) for k in range(n)]
@@ -422,6 +468,90 @@ class Builder:
                 self.add(op_sqr12(self.F, self.F))
             self.add(op_mul_line(self.F, self.F, L(s)))
 
+    # ---- Miller loop with combined lines (the 64-pair programs of k_wave64)
+    def miller_c(self, modes):
+        """Two pairs, 64 lane pairs per check.  Per step the two lines are multiplied together first
+        (op_mul_ll, 9 products, beside f^2's 21) and f takes their product in one 30-product stage
+        (op_mul_fl): f costs two stages per step where multiplying the lines in one by one costs three.
+        A WALK side keeps T in homogeneous projective coordinates with Zk = 12 xi Z (miller1's
+        formulas: a doubling is two product levels instead of three) and affine P, so its line needs no
+        Z^3 scaling; a TABLE side reads the k_oct_prep lines as in miller().  The lines are pairing
+        0.14's up to Fp2 factors, which the final exponentiation removes."""
+        steps = []
+        for b in range(62, -1, -1):
+            steps.append("D")
+            if (X_ABS >> b) & 1:
+                steps.append("A")
+        assert len(steps) == 68
+
+        def S(side, fld):
+            return "S%d_%s" % (side, fld)
+
+        def L(side, s):
+            return ["L%d_%d_%d" % (side, s % 2, c) for c in range(3)]
+
+        for side in (0, 1):
+            if modes[side] == "W":
+                self.add(Op("NONE", [], [Out("W%d_ZK" % side, [("K12XI", 1, 0)])], name="zk0"))
+
+        def walk(side, s):
+            T = lambda n: "W%d_%s" % (side, n)
+            TX, TY, TZ, XP, YP, QX, QY = (S(side, f) for f in ("TX", "TY", "TZ", "XP", "YP", "QX", "QY"))
+            ZK = T("ZK")
+            l = L(side, s)
+            if modes[side] == "T":
+                raw = ["R%d_%d_%d" % (side, s % 2, c) for c in range(3)]
+                self.add(Op("TLOAD", tload=(side, s, raw[0], raw), name="tload"))
+                self.add(Op("M1", [[Prod(raw[1], XP)], [Prod(raw[2], YP)]],
+                            [Out(l[0], [(raw[0], 1, 0)], gate=side, default="ONE"),
+                             Out(l[1], [(P_(0), 1, 0)], gate=side), Out(l[2], [(P_(1), 1, 0)], gate=side)],
+                            name="tbl"))
+                return
+            if steps[s] == "D":
+                self.add(Op("M1", [[Prod(TX, TX)], [Prod(TY, TY)], [Prod(TZ, ZK)], [Prod(TX, TY)], [Prod(TY, TZ)],
+                                   [Prod(TY, ZK)]],
+                            [Out(T("LC1"), [(P_(0), -3, 0)]), Out(T("B"), [(P_(1), 1, 0)]),
+                             Out(T("BFM"), [(P_(1), 1, 0), (P_(2), -3, 0)]), Out(T("BFP"), [(P_(1), 1, 0), (P_(2), 3, 0)]),
+                             Out(T("E2"), [(P_(2), 2, 0)]), Out(T("E6"), [(P_(2), 6, 0)]), Out(T("XY"), [(P_(3), 1, 0)]),
+                             Out(T("YZ"), [(P_(4), 1, 0)]), Out(T("LC4"), [(P_(4), 2, 0)]), Out(T("YZK"), [(P_(5), 1, 0)]),
+                             Out(l[0], [(P_(1), 1, 0), (P_(2), -1, 0)], gate=side, default="ONE")], name="hdbl1"))
+                self.add(Op("M1", [[Prod(T("XY"), T("BFM"))], [Prod(T("BFP"), T("BFP"))], [Prod(T("E2"), T("E6"))],
+                                   [Prod(T("B"), T("YZ"))], [Prod(T("B"), T("YZK"))], [Prod(T("LC1"), XP)],
+                                   [Prod(T("LC4"), YP)]],
+                            [Out(TX, [(P_(0), -2, 0)]), Out(TY, [(P_(2), 1, 0), (P_(1), -1, 0)]),
+                             Out(TZ, [(P_(3), -8, 0)]), Out(ZK, [(P_(4), -8, 0)]),
+                             Out(l[1], [(P_(5), 1, 0)], gate=side), Out(l[2], [(P_(6), 1, 0)], gate=side)],
+                            name="hdbl2"))
+            else:
+                self.add(Op("M1", [[Prod(QY, TZ)], [Prod(QX, TZ)]],
+                            [Out(T("TH"), [(TY, 1, 0), (P_(0), -1, 0)]), Out(T("LA"), [(TX, 1, 0), (P_(1), -1, 0)])],
+                            name="hadd1"))
+                self.add(Op("M1", [[Prod(T("TH"), T("TH"))], [Prod(T("LA"), T("LA"))], [Prod(T("TH"), QX)],
+                                   [Prod(T("LA"), QY)], [Prod(T("TH"), XP)], [Prod(T("LA"), YP)]],
+                            [Out(T("C"), [(P_(0), 1, 0)]), Out(T("D"), [(P_(1), 1, 0)]),
+                             Out(l[0], [(P_(2), 1, 0), (P_(3), -1, 0)], gate=side, default="ONE"),
+                             Out(l[1], [(P_(4), -1, 0)], gate=side), Out(l[2], [(P_(5), 1, 0)], gate=side)],
+                            name="hadd2"))
+                self.add(Op("M1", [[Prod(T("LA"), T("D"))], [Prod(TZ, T("C"))], [Prod(TX, T("D"))]],
+                            [Out(T("E"), [(P_(0), 1, 0)]), Out(T("G"), [(P_(2), 1, 0)]),
+                             Out(T("H"), [(P_(0), 1, 0), (P_(1), 1, 0), (P_(2), -2, 0)])], name="hadd3"))
+                self.add(Op("M1", [[Prod(T("LA"), T("H"))], [Prod(T("TH"), T("G"), d=T("H"), sd=-1)], [Prod(TY, T("E"))],
+                                   [Prod(TZ, T("E"))], [Prod(ZK, T("E"))]],
+                            [Out(TX, [(P_(0), 1, 0)]), Out(TY, [(P_(1), 1, 0), (P_(2), -1, 0)]),
+                             Out(TZ, [(P_(3), 1, 0)]), Out(ZK, [(P_(4), 1, 0)])], name="hadd4"))
+
+        LL = ["LL%d" % k for k in LL_POS] + ["XLL%d" % k for k in LL_POS[1:]]
+        for side in (0, 1):
+            walk(side, 0)
+        for s, typ in enumerate(steps):
+            if s + 1 < len(steps):
+                for side in (0, 1):
+                    walk(side, s + 1)
+            if typ == "D" and s > 0:
+                self.add(op_sqr12(self.F, self.F))
+            self.add(op_mul_ll(LL, L(0, s), L(1, s)))
+            self.add(op_mul_fl(self.F, self.F, LL))
+
     # ---- final exponentiation (k_pair.hip h_final_exp, the chain of pairing.hpp final_exp_x3)
     def final_exp(self):
         F = self.F
@@ -450,7 +580,7 @@ class Builder:
                     name="inv5"))
         self.add(op_mul_fp6(X1, R, ti))                 # f1 = f^(p^6 - 1)
         self.add(op_frob2(X2, X1))
-        self.add(op_mul12(G, X2, X1))                   # g = f1^(p^2 + 1)
+        self.add(self.mul12(G, X2, X1))                   # g = f1^(p^2 + 1)
 
         def exp(dst, base, plus1, conj_out):
             e = X_ABS + (1 if plus1 else 0)
@@ -467,24 +597,24 @@ class Builder:
                             self.add(op_cyclo(dst, src if q == 0 else dst, conj_out=conj_out and last))
                     src, run = dst, 0
                 if bit:
-                    self.add(op_mul12(dst, dst, base, conj_out=conj_out and k == 0))
+                    self.add(self.mul12(dst, dst, base, conj_out=conj_out and k == 0))
 
         if self.cyc_runs:
             self.add(op_cycrun(X1, G, 1))               # cyclo(g) g, needed for w
         else:
             self.add(op_cyclo(X1, G))
-        self.add(op_mul12(X1, X1, G))
+        self.add(self.mul12(X1, X1, G))
         exp(T, G, True, True)                           # t = g^(x-1)
         exp(A, T, True, True)                           # a = t^(x-1)
         exp(T, A, False, True)                          # t = a^x
         self.add(op_frob1(FR, A))
-        self.add(op_mul12(B, T, FR))                    # b = a^x frob1(a)
+        self.add(self.mul12(B, T, FR))                    # b = a^x frob1(a)
         self.add(op_frob2(X2, B))
-        self.add(op_mul12(X2, X2, B, negb_odd=True))    # frob2(b) conj(b)
-        self.add(op_mul12(X1, X2, X1))                  # w
+        self.add(self.mul12(X2, X2, B, negb_odd=True))    # frob2(b) conj(b)
+        self.add(self.mul12(X1, X2, X1))                  # w
         exp(T, B, False, True)                          # b^x
         exp(A, T, False, True)                          # c = (b^x)^x
-        self.add(op_mul12(self.group("E"), A, X1))      # e = c w
+        self.add(self.mul12(self.group("E"), A, X1))      # e = c w
         return self.group("E")
 
     # ---- F <- F * G: the product of partial Miller values (the split master check of
@@ -677,7 +807,8 @@ def encode(b, stages):
                 raw = op.tload[3]
                 assert [S[r] for r in raw] == [S[raw[0]] + k for k in range(3)]
                 h3 |= (1 | (op.tload[1] << 1) | (S[raw[0]] << 8)) << (16 * side)
-        h0 |= (st.npairs << 16) | (st.nouts << 22)
+        assert st.npairs < 128 and st.nouts < 128
+        h0 |= (st.npairs << 16) | (st.nouts << 23)
         hdrs.extend([h0, pcache[key], acache[akey], h3])
     return hdrs, pdesc, adesc
 
@@ -835,7 +966,7 @@ def _run(mem, act, tables, hdrs, pdesc, adesc, names=None):
         h0, po, ao, h3 = hdrs[4 * st:4 * st + 4]
         kind, j1, j2 = h0 & 3, (h0 >> 2) & 7, (h0 >> 5) & 7
         special = (h0 >> 12) & 0xF
-        npairs, nouts = (h0 >> 16) & 63, (h0 >> 22) & 63
+        npairs, nouts = (h0 >> 16) & 127, (h0 >> 23) & 127
         K = 2 if kind == 1 else 1
         new = {}
         if special == SPECIAL_CYC:
@@ -986,48 +1117,68 @@ def allocate(b, stages):
     return mapping
 
 
-def build():
+MODES64 = ["WW", "WT", "TW", "TT"]  # the 64-pair set (k_wave64): plain two-pair checks only
+COMBINED32 = ("TT",)                # 32-pair modes whose Miller program uses the combined lines
+
+
+def build(npairs=32):
     """One program per WALK/TABLE combination for the Miller part and one final exponentiation,
-    each scheduled into stages and then given physical LDS slots by live range (allocate)."""
-    out = {"variants": {}}
-    fe = Builder("fe")
-    fe.final_exp()
-    fe_stages = schedule(fe.ops)
-    fe.slots = allocate(fe, fe_stages)
-    fe_enc = encode(fe, fe_stages)
-    nslots = max(fe.slots.values()) + 1
-    for m in MODES:
-        b = Builder(m)
-        if m == "W1J":
-            b.miller1()
-        else:
-            b.miller(tuple(m))
-        st = schedule(b.ops)
-        b.slots = allocate(b, st)
-        nslots = max(nslots, max(b.slots.values()) + 1)
-        out["variants"][m] = {"miller": encode(b, st), "fe": fe_enc, "slots": b.slots, "slots_fe": fe.slots,
-                              "nstages_miller": len(st), "nstages_fe": len(fe_stages),
-                              "stages_miller": st, "stages_fe": fe_stages}
-    mf = Builder("mulf")
-    mf.mulf()
-    mf_stages = schedule(mf.ops)
-    mf.slots = allocate(mf, mf_stages)
-    mf_enc = encode(mf, mf_stages)
-    for v in out["variants"].values():
-        v["mulf"] = mf_enc
-    out["mulf"] = mf_enc
-    out["nstages_mulf"] = len(mf_stages)
-    out["nslots"] = nslots
-    out["slots"] = fe.slots
-    return out
+    each scheduled into stages and then given physical LDS slots by live range (allocate).
+    npairs = 32: k_wave's set (one wave per check); mode TT takes the combined-line Miller program
+    (miller_c: 138 stages instead of 200 -- two tabled sides fit 32 pairs), the walking modes keep
+    miller() (the homogeneous walk's levels beside f^2 and the line product need more than 32).
+    npairs = 64: k_wave64's set (two waves per check), every mode on miller_c (149 stages for a
+    walked side instead of 210-211); the final exponentiation is the 32-pair one (its Fp12 products
+    stay M2: one-product pairs would need more than 7 assembly terms per output)."""
+    global NPAIRS
+    saved, NPAIRS = NPAIRS, 32
+    try:
+        out = {"variants": {}, "npairs": npairs}
+        fe = Builder("fe")
+        fe.final_exp()
+        fe_stages = schedule(fe.ops)
+        mf = Builder("mulf")
+        mf.mulf()
+        mf_stages = schedule(mf.ops)
+        NPAIRS = npairs
+        fe.slots = allocate(fe, fe_stages)
+        fe_enc = encode(fe, fe_stages)
+        nslots = max(fe.slots.values()) + 1
+        for m in (MODES if npairs == 32 else MODES64):
+            b = Builder(m)
+            if m == "W1J":
+                b.miller1()
+            elif npairs == 64 or m in COMBINED32:
+                b.miller_c(tuple(m))
+            else:
+                b.miller(tuple(m))
+            st = schedule(b.ops)
+            b.slots = allocate(b, st)
+            nslots = max(nslots, max(b.slots.values()) + 1)
+            out["variants"][m] = {"miller": encode(b, st), "fe": fe_enc, "slots": b.slots, "slots_fe": fe.slots,
+                                  "nstages_miller": len(st), "nstages_fe": len(fe_stages),
+                                  "stages_miller": st, "stages_fe": fe_stages}
+        mf.slots = allocate(mf, mf_stages)
+        mf_enc = encode(mf, mf_stages)
+        for v in out["variants"].values():
+            v["mulf"] = mf_enc
+        out["mulf"] = mf_enc
+        out["nstages_mulf"] = len(mf_stages)
+        out["nslots"] = nslots
+        out["slots"] = fe.slots
+        return out
+    finally:
+        NPAIRS = saved
 
 
-def emit(out, path):
+def emit(out, path, ns="hbw"):
     slots = out["slots"]
+    modes = MODES if out["npairs"] == 32 else MODES64
     lines = ["// Generated by tools/gen_wave_prog.py -- do not edit.  Stage programs of the wave-per-check",
-             "// pairing kernel (k_wave.hip): 4 u32 header per stage, u64 product descriptors, 8 x u16",
-             "// assembly descriptors (formats in tools/gen_wave_prog.py).",
-             "#pragma once", "#include <stdint.h>", "namespace hbw {",
+             "// pairing kernel (k_wave.hip; %d lane pairs per check): 4 u32 header per stage, u64 product" % out["npairs"],
+             "// descriptors, 8 x u16 assembly descriptors (formats in tools/gen_wave_prog.py).",
+             "#pragma once", "#include <stdint.h>", "namespace %s {" % ns,
+             "constexpr int WP_NPAIRS = %d;" % out["npairs"],
              "constexpr int WP_NSLOTS = %d;" % out["nslots"],
              "constexpr int WP_F = %d;" % slots["F0"],
              "constexpr int WP_E = %d;" % slots["E0"],
@@ -1052,17 +1203,19 @@ def emit(out, path):
 
     fe_off, fe_n = append(fe)
     mf_off, mf_n = append(out["mulf"])
-    for m in MODES:
+    for m in modes:
         mo, mn = append(out["variants"][m]["miller"])
         info.append((mo, mn))
     lines.append("constexpr int WP_FE_OFF = %d, WP_FE_N = %d;" % (fe_off, fe_n))
     lines.append("// F <- F * G with G in side 0's slots XP YP QX QY TX TY (product of partial Miller values)")
     lines.append("constexpr int WP_MULF_OFF = %d, WP_MULF_N = %d;" % (mf_off, mf_n))
     lines.append("// Miller programs: WALK/TABLE for side 0 and side 1 -> index (side0 is TABLE) * 2 + (side1 is TABLE);")
-    lines.append("// index 4: both sides WALK with Jacobian P (XP = X Z, YP = Y, ZP = Z^3); 5: side 0 only, the same")
-    lines.append("// Jacobian P, homogeneous walk (one pair per wave)")
-    lines.append("constexpr int WP_MILLER_OFF[6] = {%s};" % ", ".join(str(i[0]) for i in info))
-    lines.append("constexpr int WP_MILLER_N[6] = {%s};" % ", ".join(str(i[1]) for i in info))
+    if out["npairs"] == 32:
+        lines.append("// index 4: both sides WALK with Jacobian P (XP = X Z, YP = Y, ZP = Z^3); 5: side 0 only, the same")
+        lines.append("// Jacobian P, homogeneous walk (one pair per wave)")
+    lines.append("constexpr int WP_NMODES = %d;" % len(modes))
+    lines.append("constexpr int WP_MILLER_OFF[%d] = {%s};" % (len(modes), ", ".join(str(i[0]) for i in info)))
+    lines.append("constexpr int WP_MILLER_N[%d] = {%s};" % (len(modes), ", ".join(str(i[1]) for i in info)))
 
     def arr(name, typ, vals, per):
         lines.append("__device__ __attribute__((aligned(16))) const %s %s[%d] = {" % (typ, name, len(vals)))
@@ -1073,18 +1226,17 @@ def emit(out, path):
     arr("WP_HDR", "uint32_t", hdr_all, 8)
     arr("WP_PDESC", "uint64_t", pd_all, 6)
     arr("WP_ADESC", "uint16_t", ad_all, 16)
-    lines.append("}  // namespace hbw")
+    lines.append("}  // namespace %s" % ns)
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 
 
 def stats(out):
     cost = {"M1": 1.0, "M2": 1.67, "SQ": 0.67, "NONE": 0.2}
-    for m in MODES:
-        v = out["variants"][m]
+    for m, v in out["variants"].items():
         c = sum(cost[s.kind] for s in v["stages_miller"]) + sum(cost[s.kind] for s in v["stages_fe"])
-        print("%s: %d Miller stages + %d final-exp stages, %.0f M1-equivalents, %d slots" % (
-            m, v["nstages_miller"], v["nstages_fe"], c, out["nslots"]))
+        print("%d pairs %s: %d Miller stages + %d final-exp stages, %.0f M1-equivalents, %d slots" % (
+            out["npairs"], m, v["nstages_miller"], v["nstages_fe"], c, out["nslots"]))
 
 
 if __name__ == "__main__":
@@ -1092,3 +1244,6 @@ if __name__ == "__main__":
     o = build()
     stats(o)
     emit(o, os.path.join(root, "hbbft_amd", "csrc", "wave_prog.inc"))
+    o64 = build(64)
+    stats(o64)
+    emit(o64, os.path.join(root, "hbbft_amd", "csrc", "wave_prog64.inc"), ns="hbw64")

@@ -9,7 +9,7 @@ sys.path.insert(0, ROOT)
 from oracle import bls12_381 as C  # noqa: E402
 from oracle import cbls  # noqa: E402
 from hbbft_amd.engine import Engine, g1_abi_from_uncompressed as g1a, g2_abi_from_uncompressed as g2a  # noqa: E402
-from hbbft_amd._lib import IMPL_PAIR, IMPL_WAVE, IMPL_OCT, IMPL_AUTO  # noqa: E402
+from hbbft_amd._lib import IMPL_PAIR, IMPL_WAVE, IMPL_OCT, IMPL_AUTO, IMPL_WAVE2  # noqa: E402
 
 sizes = [int(x) for x in sys.argv[1:]] or [1, 1024, 4096, 8192]
 eng = Engine(0)
@@ -33,8 +33,8 @@ for n in sizes:
     eng.set_pairing_impl(IMPL_PAIR)
     ref = eng.verify_sig_shares(*a)
     row = ["n=%d" % n]
-    for name, impl in (("wave", IMPL_WAVE), ("oct", IMPL_OCT), ("auto", IMPL_AUTO)):
-        if impl == IMPL_WAVE and n > 4096:
+    for name, impl in (("wave2", IMPL_WAVE2), ("wave", IMPL_WAVE), ("oct", IMPL_OCT), ("auto", IMPL_AUTO)):
+        if impl in (IMPL_WAVE, IMPL_WAVE2) and n > 4096:
             continue
         eng.set_pairing_impl(impl)
         assert eng.verify_sig_shares(*a) == ref, (name, n)
