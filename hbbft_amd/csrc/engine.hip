@@ -187,6 +187,8 @@ hbl::PairSideDesc offset_side(const hbl::PairSideDesc& d, size_t off) {
   return o;
 }
 
+#define HBH_WAVE_TT_MIN 1024  // WAVE calls that table two shared G2 sides (launch_pair)
+
 // HBH_IMPL_WAVE2 (two waves per check) takes plain checks only; the split master check's modes
 // (Miller-only, Jacobian P, one side) run on WAVE
 hipError_t wave2_verify(hipStream_t s, int n, const hbl::PairSideDesc& a, const hbl::PairSideDesc& b, int flags,
@@ -247,9 +249,14 @@ int launch_pair(hbh_engine* e, hipStream_t s, int impl, size_t n, const void* d_
   hbl::PairSideDesc sd[2] = {{d_p1, d_q1, nullptr, nullptr, d_i1, nq1}, {d_p2, d_q2, nullptr, nullptr, d_i2, nq2}};
   DevBuf* tab[2] = {&e->ptab[slot][0], &e->ptab[slot][1]};
   DevBuf* inf[2] = {&e->pinf[slot][0], &e->pinf[slot][1]};
+  const bool tab_ok[2] = {sd[0].idx && sd[0].nq * 4 <= n, sd[1].idx && sd[1].nq * 4 <= n};
   for (int k = 0; k < 2; k++) {
-    // WAVE walks every side: a table costs a serial 68-step walk (k_oct_prep) before the first check
-    if (!sd[k].idx || sd[k].nq * 4 > n || impl == HBH_IMPL_WAVE || impl == HBH_IMPL_WAVE2) continue;
+    // WAVE2 walks every side: a table costs a serial 68-step walk (k_oct_prep, ~0.5 ms) before the
+    // first check.  WAVE tables both sides of a call of >= HBH_WAVE_TT_MIN checks when both are
+    // shared (decryption shares: H_uv and W per ciphertext): its TT program takes 138 Miller stages
+    // where walking both sides takes 211 (round 6); one walked side gains nothing (TW: 210).
+    if (!tab_ok[k] || impl == HBH_IMPL_WAVE2) continue;
+    if (impl == HBH_IMPL_WAVE && !(tab_ok[0] && tab_ok[1] && n >= HBH_WAVE_TT_MIN)) continue;
     HBH_CHECK(tab[k]->ensure(hbl::pair_table_bytes(sd[k].nq)));
     HBH_CHECK(inf[k]->ensure(sd[k].nq));
     hipEvent_t t = e->timer.begin(s, HBH_STAGE_PREPARE, e->profiling);

@@ -179,3 +179,30 @@ def test_config3_10000_acks(engine):
     assert v == bytes(0 if a in bad else 1 for a in range(len(vals)))
     for a in (0, 3, 4999, 9999):
         assert (cbls.bivar_evaluate(t, parts[pidx[a]], xs[a], ys[a]) == cbls.g1_mul(G1, vals[a])) == bool(v[a])
+
+
+@pytest.mark.parametrize("n", [1024, 2048])
+def test_dec_shares_wave_tabled_sides(engine, n):
+    """Round 6: a WAVE call of >= 1,024 checks whose two G2 sides are both shared (decryption shares:
+    H_uv and W per ciphertext) tables both and runs the combined-line TT program (138 Miller stages);
+    WAVE, WAVE2 (both sides walked) and PAIR give the construction's verdicts."""
+    from hbbft_amd._lib import IMPL_PAIR
+    rng = random.Random(100 + n)
+    coeffs, sks, pks, mpk = keyset(engine, rng, N, T)
+    ncts = n // N
+    rs = [rng.randrange(1, R) for _ in range(ncts)]
+    hs = [rng.randrange(1, R) for _ in range(ncts)]
+    us = engine.g1_mul([G1] * ncts, rs)
+    huv = engine.g2_mul([G2] * ncts, hs)
+    ws = engine.g2_mul([G2] * ncts, [h * r % R for h, r in zip(hs, rs)])
+    bad = {c * N + (c * 13) % N for c in range(ncts)} | {5, n - 2}
+    shares = engine.g1_mul([us[i // N] for i in range(n)],
+                           [rng.randrange(1, R) if i in bad else sks[i % N] for i in range(n)])
+    want = bytes(0 if i in bad else 1 for i in range(n))
+    for impl in (IMPL_WAVE, IMPL_WAVE2, IMPL_PAIR):
+        engine.set_pairing_impl(impl)
+        try:
+            v = engine.verify_dec_shares(shares, [pks[i % N] for i in range(n)], huv, ws, [i // N for i in range(n)])
+        finally:
+            engine.set_pairing_impl(IMPL_AUTO)
+        assert v == want, impl
