@@ -1275,6 +1275,13 @@ def run_epoch_bench(args, eng, world, rank, dev):
             "outputs_ok": ok, "phase_ms": phases, "host_vs_gpu": host_gpu,
             "engine_calls_per_epoch": sum(r.engine_calls for r in results) / len(results),
             "checks_drained_per_epoch": drained / len(results), "checks_consumed_per_epoch": consumed,
+            #  checks verified on the GPU that no instance read: shares pre-verified
+            # for instances that terminated first (the reference never verifies those,
+            # threshold_sign.rs:182-184, threshold_decrypt.rs:183-185) -- latency hiding, priced at the
+            # drains' average kernel time per check
+            "checks_unconsumed_per_epoch": drained / len(results) - consumed,
+            "unconsumed_gpu_ms_per_epoch_est": (kern.get("pairing", 0.0) + kern.get("line_tables", 0.0))
+            * max(0.0, 1.0 - consumed * len(results) / max(drained, 1)),
             "roofline": dict(main_k, bound="valu-int", unit="T MAD/s (v_mad_u64_u32 32x32->64)", traffic=None,
                              traffic_note="the drains mix kernels at varying sizes; their per-launch HBM is in "
                                           "profiles/r04/pmc_traffic.json (by_source wave4k: k_wave 4,096 checks, "

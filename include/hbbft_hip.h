@@ -350,7 +350,7 @@ int hbh_fr_poly_eval(size_t npoly, size_t ncoef, const uint8_t* coeffs, size_t n
 #define HBH_IMPL_QUAD 6
 #define HBH_IMPL_OCT 7
 #define HBH_IMPL_WAVE2 8
-#define HBH_AUTO_WAVE2_MAX 256  /* AUTO: WAVE2 up to here (two waves per check), then WAVE */
+#define HBH_AUTO_WAVE2_MAX 512  /* AUTO: WAVE2 up to here (two waves per check), then WAVE (profiles/r06/latency_c6.txt) */
 #define HBH_AUTO_WAVE_MAX 4096
 #define HBH_AUTO_OCT_MAX 8192
 #define HBH_AUTO_QUAD_MAX 16384

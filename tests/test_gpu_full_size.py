@@ -72,7 +72,7 @@ def test_config1_65536_sig_shares(engine, sign_batch, impl):
         assert cbls.verify_g2(b["pks"][i % N], b["sigs"][i], b["hashes"][i // N]) == bool(v[i]), i
 
 
-@pytest.mark.parametrize("n", [256, 320, 4096, 4160, 8192, 8256, 16384, 16448, 32768, 32832, 49152, 49216],
+@pytest.mark.parametrize("n", [512, 576, 4096, 4160, 8192, 8256, 16384, 16448, 32768, 32832, 49152, 49216],
                          ids=["wave2_max", "wave_min", "wave_max", "oct_min", "oct_max", "quad_min", "quad_max",
                               "pair_min", "split_lo", "split_min", "split_max", "pair2_min"])
 def test_config1_at_auto_thresholds(engine, sign_batch, n):
