@@ -45,11 +45,12 @@ ACK_LANE_MIN = 65536                            # HBH_ACK_LANE_MIN (include/hbbf
 MAD_PEAK_MEASURED = 38.12                       # T MAD/s at 8 waves/SIMD
 MAD_CEILING_BY_WAVES = {1: 17.48, 2: 33.64, 4: 35.20, 8: 38.12}
 MAD_PEAK_THEORETICAL = 256 * 4 * 32 * 2.4e9 / 2 / 1e12   # 256 CU x 4 SIMD32 x 2.4 GHz, half rate = 39.32
-IMPLS = {"auto": 3, "pair": 4, "wave": 5, "quad": 6, "oct": 7}   # HBH_IMPL_* (include/hbbft_hip.h)
+IMPLS = {"auto": 3, "pair": 4, "wave": 5, "quad": 6, "oct": 7, "wave2": 8}   # HBH_IMPL_* (include/hbbft_hip.h)
 PAIR_SIGN = "hbs::k_pair_verify<false, true, 2>"
 PAIR_DECRYPT = "hbs::k_pair_verify<false, false, 0>"
 KERNEL_NAMES = {"pair": PAIR_SIGN,
                 "wave": "hbs::k_wave (one wave per check)",
+                "wave2": "hbs64::k_wave (two waves per check)",
                 "quad": "hbs::k_quad_verify<false, true, 2>",
                 "oct": "hbs::k_oct_verify<false, true, 2>",
                 "auto": PAIR_SIGN,
@@ -533,7 +534,7 @@ def main():
     ap.add_argument("--no-node-round", action="store_true",
                     help="dkg workload: skip the one-node SyncKeyGen round (node_round)")
     ap.add_argument("--streams", type=int, default=2, help="sign workload: streams the consecutive batches alternate on")
-    ap.add_argument("--impl", choices=["pair", "wave", "quad", "oct", "auto"], default="auto",
+    ap.add_argument("--impl", choices=["pair", "wave", "quad", "oct", "auto", "wave2"], default="auto",
                     help="pairing implementation (hbh_engine_set_pairing_impl)")
     ap.add_argument("--profile-epoch", default=None, metavar="FILE",
                     help="epoch workload: cProfile the timed epochs (main thread), pstats text to FILE")
