@@ -10,6 +10,10 @@
 #include "wire.hpp"
 #include "sqrt_chain.inc"
 
+#ifndef HBH_G1_WAVES_PER_SIMD
+#define HBH_G1_WAVES_PER_SIMD 2  // A/B: 1 (512 registers, no spills, half the waves in flight)
+#endif
+
 namespace hb {
 
 // canonical words a > b
@@ -84,41 +88,64 @@ __device__ __forceinline__ bool g2_in_subgroup(const Fp2& x, const Fp2& y) {
 }
 
 // ---------------------------------------------------------------------------- decompression
-__global__ void __launch_bounds__(256) k_g1_decompress(int n, const uint32_t* __restrict__ xw,
+// G1: two waves per 64 points (k_g1_decompress, 128 threads).  The subgroup test does not need y:
+// (x, y) -> (u^2 x, u^3 y) with u = y maps E: y^2 = x^3 + 4 isomorphically onto E_u: Y^2 = X^3 + 4 rhs^3
+// (rhs = x^3 + 4 = y^2) and sends (x, y) to P' = (rhs x, rhs^2) -- known from x alone.  The map
+// commutes with scalar multiplication and with phi (beta scales X by the same u^2), and the a = 0
+// Jacobian formulas never read b, so phi(P') == [-x^2] P'  <=>  phi(P) == [-x^2] P.  Wave 0 takes the
+// square root (375 squarings + 86 products) while wave 1 runs the subgroup test on P' (two [|x|]
+// chains): each point's serial chain is the longer of the two instead of their sum, and 65,536
+// points are two waves per SIMD instead of one (the decoder is issue-bound at one wave per SIMD:
+// profiles/r06/c3_wire/decode_pmc_sq.csv, ~5.1 cycles per VALU instruction).  When rhs is not a
+// square, P' lies on a twist and wave 1's answer is discarded with the point.
+__global__ void __launch_bounds__(128, HBH_G1_WAVES_PER_SIMD) k_g1_decompress(int n, const uint32_t* __restrict__ xw,
                                                        const uint8_t* __restrict__ flags, uint32_t* __restrict__ out,
                                                        uint8_t* __restrict__ ok) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t* o = out + (size_t)i * G1_WORDS;
-  const uint8_t f = flags[i];
+  __shared__ uint8_t in_group[64];
+  const int lane = threadIdx.x & 63, role = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  const uint8_t f = live ? flags[i] : hbl::WIRE_REJECT;
+  uint32_t x[12];
+  for (int k = 0; k < 12; k++) x[k] = live ? xw[(size_t)i * 12 + k] : 0u;
+  uint32_t p[12];
+  for (int k = 0; k < 12; k++) p[k] = PM2_W[k];
+  p[0] += 2;
+  const bool try_point = !(f & hbl::WIRE_INFINITY) && !(f & hbl::WIRE_REJECT) && words_gt(p, x, 12);  // x < p
+  Fp xm = fp_zero(), rhs = fp_zero();
+  if (try_point) {
+    xm = fp_from_words(x);
+    rhs = fp_add(fp_mul(fp_sqr(xm), xm), fp_const(B1_M));
+  }
+  if (role == 1) {  // the subgroup test on P' = (rhs x, rhs^2)
+    bool g = false;
+    if (try_point) g = g1_in_subgroup(fp_mul(rhs, xm), fp_sqr(rhs));
+    in_group[lane] = g ? 1 : 0;
+  }
+  __syncthreads();
+  if (role == 1 || !live) return;
   bool valid = false;
-  uint32_t x[12], y[12];
-  for (int k = 0; k < 12; k++) x[k] = xw[(size_t)i * 12 + k], y[k] = 0;
+  uint32_t y[12];
+  for (int k = 0; k < 12; k++) y[k] = 0;
   if (f & hbl::WIRE_INFINITY) {
     valid = true;  // the point at infinity (all-zero ABI words)
     for (int k = 0; k < 12; k++) x[k] = 0;
-  } else if (!(f & hbl::WIRE_REJECT)) {
-    uint32_t p[12];
-    for (int k = 0; k < 12; k++) p[k] = PM2_W[k];
-    p[0] += 2;
-    if (words_gt(p, x, 12)) {  // x < p
-      const Fp xm = fp_from_words(x);
-      const Fp rhs = fp_add(fp_mul(fp_sqr(xm), xm), fp_const(B1_M));
-      Fp ym = fp_mul(rhs, fp_pow_pm3d4(rhs));  // rhs^((p+1)/4)
-      if (fp_eq(fp_sqr(ym), rhs)) {
-        // "greatest" = y > p - y, i.e. y > (p - 1) / 2
+  } else if (try_point) {
+    Fp ym = fp_mul(rhs, fp_pow_pm3d4(rhs));  // rhs^((p+1)/4)
+    if (fp_eq(fp_sqr(ym), rhs)) {
+      // "greatest" = y > p - y, i.e. y > (p - 1) / 2
+      fp_to_words(ym, y);
+      uint32_t half[12];
+      for (int k = 0; k < 12; k++) half[k] = (p[k] >> 1) | (k < 11 ? (p[k + 1] << 31) : 0u);
+      const bool greatest = words_gt(y, half, 12);
+      if (greatest != ((f & hbl::WIRE_GREATEST) != 0)) {
+        ym = fp_neg(ym);
         fp_to_words(ym, y);
-        uint32_t half[12];
-        for (int k = 0; k < 12; k++) half[k] = (p[k] >> 1) | (k < 11 ? (p[k + 1] << 31) : 0u);
-        const bool greatest = words_gt(y, half, 12);
-        if (greatest != ((f & hbl::WIRE_GREATEST) != 0)) {
-          ym = fp_neg(ym);
-          fp_to_words(ym, y);
-        }
-        valid = g1_in_subgroup(xm, ym);
       }
+      valid = in_group[lane] != 0;
     }
   }
+  uint32_t* o = out + (size_t)i * G1_WORDS;
   for (int k = 0; k < 12; k++) {
     o[k] = valid ? x[k] : 0u;
     o[12 + k] = valid ? y[k] : 0u;
@@ -248,7 +275,7 @@ hipError_t wire_parse(hipStream_t s, int n, int nfe, const uint8_t* in, uint32_t
 
 hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hb::k_g1_decompress, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, xw, flags,
+  hipLaunchKernelGGL(hb::k_g1_decompress, dim3((unsigned)((n + 63) / 64)), dim3(128), 0, s, n, xw, flags,
                      (uint32_t*)out, ok);
   return hipGetLastError();
 }
