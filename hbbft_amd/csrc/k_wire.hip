@@ -117,20 +117,17 @@ __global__ void __launch_bounds__(128, HBH_G1_WAVES_PER_SIMD) k_g1_decompress(in
     xm = fp_from_words(x);
     rhs = fp_add(fp_mul(fp_sqr(xm), xm), fp_const(B1_M));
   }
+  bool valid = false;
+  uint32_t y[12];
+  for (int k = 0; k < 12; k++) y[k] = 0;
   if (role == 1) {  // the subgroup test on P' = (rhs x, rhs^2)
     bool g = false;
     if (try_point) g = g1_in_subgroup(fp_mul(rhs, xm), fp_sqr(rhs));
     in_group[lane] = g ? 1 : 0;
-  }
-  __syncthreads();
-  if (role == 1 || !live) return;
-  bool valid = false;
-  uint32_t y[12];
-  for (int k = 0; k < 12; k++) y[k] = 0;
-  if (f & hbl::WIRE_INFINITY) {
+  } else if (f & hbl::WIRE_INFINITY) {
     valid = true;  // the point at infinity (all-zero ABI words)
     for (int k = 0; k < 12; k++) x[k] = 0;
-  } else if (try_point) {
+  } else if (try_point) {  // the square root, beside the other wave's subgroup test
     Fp ym = fp_mul(rhs, fp_pow_pm3d4(rhs));  // rhs^((p+1)/4)
     if (fp_eq(fp_sqr(ym), rhs)) {
       // "greatest" = y > p - y, i.e. y > (p - 1) / 2
@@ -142,9 +139,12 @@ __global__ void __launch_bounds__(128, HBH_G1_WAVES_PER_SIMD) k_g1_decompress(in
         ym = fp_neg(ym);
         fp_to_words(ym, y);
       }
-      valid = in_group[lane] != 0;
+      valid = true;  // on the curve; the subgroup verdict joins after the barrier
     }
   }
+  __syncthreads();
+  if (role == 1 || !live) return;
+  if (try_point) valid = valid && in_group[lane] != 0;
   uint32_t* o = out + (size_t)i * G1_WORDS;
   for (int k = 0; k < 12; k++) {
     o[k] = valid ? x[k] : 0u;
