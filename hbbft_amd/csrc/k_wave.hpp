@@ -86,10 +86,13 @@ HP_D Fp operand(const uint32_t* sm, int h, int a, int b, int scode, int negb, in
 }
 
 // own component of sum_t x_t * y_t (Fp2, lane-pair split of pfp.hpp h_mul_l), one reduction.
-// One wave per SIMD runs this kernel, so nothing hides a MAD's latency but the wave's own ILP: each
-// column is summed in WV_NACC independent int64 chains, joined before the Montgomery digit.
+// Each column may be summed in WV_NACC independent int64 chains, joined before the Montgomery digit.
+// One chain is fastest (round 6 A/B, profiles/r06/ab_nacc_dpp.txt: single check 1.62 -> 1.53 ms,
+// 4,096 checks 5.50 -> 5.18 ms against four): at one wave per SIMD a dependent v_mad_i64_i32 costs
+// ~11 cycles against ~9 for independent ones (tools/ubench_issue.hip), while every extra chain costs
+// a two-instruction 64-bit join per column -- the wave is issue-bound, not latency-bound.
 #ifndef WV_NACC
-#define WV_NACC 4
+#define WV_NACC 1
 #endif
 template <int K>
 HP_D Fp wv_mul(const Fp (&x)[K], const Fp (&y)[K]) {
@@ -268,7 +271,9 @@ HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, boo
 //   X = 3 (sA + xi sB) - 2 L,  Y = 3 (sAB - sA - sB) + 2 L,  Z = 3 xi (sAB - sA - sB) + 2 L
 // with L the input at the output's position.  Lane row g (16 lanes) runs one Fp4 squaring: lane quads
 // 0 / 1 hold A / B (own Fp2 component), quad 2 squares A + B; the squares and the two inputs move by lane shuffles (ds_bpermute) inside
-// the wave -- no LDS slot traffic and no barrier per squaring.  Row 0
+// the wave -- no LDS slot traffic and no barrier per squaring (DPP row shifts instead of the
+// ds_bpermute exchanges inside a row measured neutral: single check -1.5 % on WAVE2, +1.8 % on WAVE,
+// profiles/r06/ab_dpp.txt).  Row 0
 // keeps (f0, f3).  Rows 1 and 2 swap roles each squaring: the row squaring (f1, f4) produces the next
 // (f2, f5) and vice versa, so squaring inputs never move; only L crosses between rows 1 and 2.
 HP_D Fp shfl_fp(const Fp& a, int src_lane) {
@@ -301,7 +306,10 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
   // lane = 16 row + 4 j + 2 rr + h: squaring j of the row, component h (rr: idle copy)
   const int h = lane & 1, rr = (lane >> 1) & 1, row = lane >> 4, j = (lane >> 2) & 3;
   const bool holder = row < 3 && j < 2;
-  const int count = (int)((w1 >> 48) & 0xFF);
+  int count = (int)((w1 >> 48) & 0xFF);
+#ifdef WV_CYC_REPEAT  // timing-only A/B builds (wrong verdicts): each run squares WV_CYC_REPEAT x as often
+  count *= WV_CYC_REPEAT;
+#endif
   const bool conj = ((w1 >> 56) & 1) != 0;
   int role = row < 3 ? row : 0;
   Fp v = fp_zero();
@@ -602,7 +610,9 @@ __global__ void __launch_bounds__(WV_THREADS) k_wave(WaveArgs a) {
         fp_to_words(ld_own(sm, WV_PROG::WP_F + pair, h), a.value_out + (size_t)i * 144 + 24 * pair + 12 * h);
       return;
     }
+#ifndef WV_FE_SKIP  // timing-only A/B builds (wrong verdicts): Miller loop without the final exponentiation
     run_stages(sm, WV_PROG::WP_FE_OFF, WV_PROG::WP_FE_N, h, pair, act0, act1, tl0, tl1);
+#endif
   }
   // e = f^(3 (p^12 - 1) / r) in slots E0..E5 (w-basis)
   bool ok = true;

@@ -37,7 +37,8 @@ for n in sizes:
         if impl in (IMPL_WAVE, IMPL_WAVE2) and n > 4096:
             continue
         eng.set_pairing_impl(impl)
-        assert eng.verify_sig_shares(*a) == ref, (name, n)
+        if not os.environ.get("HBH_PROBE_NOCHECK"):  # timing-only A/B libraries give wrong verdicts
+            assert eng.verify_sig_shares(*a) == ref, (name, n)
         eng.set_profiling(True)
         for _ in range(3):
             eng.verify_sig_shares(*a)
