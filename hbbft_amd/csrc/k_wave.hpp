@@ -64,6 +64,27 @@ HP_D void st_own(uint32_t* sm, int slot, int h, const Fp& a) {
   }
 }
 
+// One carry step on every limb at once: limb i keeps its low 28 bits plus the carry out of limb i - 1
+// (taken from limb i - 1's value BEFORE this step).  For |limb| < 2^31 the result has limbs in
+// [-8, 2^28 + 8) and the same value -- "almost normalised", which is all the product bounds need
+// (sfp.hpp (M): |limb| <= 2^29), at the latency of one step instead of fp_norm's 13 dependent ones.
+#ifndef WV_PAR_CARRY
+#define WV_PAR_CARRY 1
+#endif
+HP_D void fp_carry1(Fp& a) {
+  if (!WV_PAR_CARRY) {  // A/B: the sequential carry chain
+    fp_norm(a);
+    return;
+  }
+  int32_t c[NL];
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) c[i] = a.l[i] >> 28;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) a.l[i] &= MASK28;
+#pragma unroll
+  for (int i = 1; i < NL; i++) a.l[i] += c[i - 1];
+}
+
 // X = sgn * (S[a] + s * S[b]); s in {0, 1, -1} (codes 0, 1, 2), sgn = -1 for neg, -1 on the odd
 // lane for conj.  Lazy limbs (|limb| < 2^29); normalised when `norm`.
 HP_D Fp operand(const uint32_t* sm, int h, int a, int b, int scode, int negb, int conjb, bool sum, bool sgnflag,
@@ -81,7 +102,7 @@ HP_D Fp operand(const uint32_t* sm, int h, int a, int b, int scode, int negb, in
 #pragma unroll
     for (int i = 0; i < NL; i++) x.l[i] = (x.l[i] ^ m) - m;
   }
-  if (norm) fp_norm(x);
+  if (norm) fp_carry1(x);  // |limb| < 2^29 -> [-2, 2^28 + 1): the y operand of wv_mul
   return x;
 }
 
@@ -227,39 +248,63 @@ HP_D void assemble(uint32_t* sm, int h, uint4 dw, int j1, int j2, bool act0, boo
     ap[i] = 0;
     at[i] = 0;
   }
+  // the seven terms' reads are written unconditionally (an unused term reads slot 0 and is never
+  // added); the compiler places them.  Forcing all seven ahead of the sums (an empty asm using each
+  // value) measured slower: single check 1.43 -> 1.48 ms (WAVE2), 1.65 -> 1.73 ms (WAVE),
+  // profiles/r06/c14_inv/ab.txt -- register pressure at two waves per SIMD.
+  Fp v[7];
+  int cf[7];
+#pragma unroll
+  for (int t = 0; t < 7; t++) {
+    const int tm = ws[1 + t];
+    int c = (tm >> 8) & 0xF;
+    c = c >= 8 ? c - 16 : c;
+    if ((tm >> 12) & h & 1) c = -c;
+    cf[t] = c;
+    v[t] = ld_own(sm, t < j1 + j2 ? (tm & 0xFF) : 0, h);
+  }
 #pragma unroll
   for (int t = 0; t < 7; t++) {
     if (t < j1 + j2) {  // uniform across the wave
-      const int tm = ws[1 + t];
-      int c = (tm >> 8) & 0xF;
-      c = c >= 8 ? c - 16 : c;
-      if ((tm >> 12) & h & 1) c = -c;
-      const Fp v = ld_own(sm, tm & 0xFF, h);
       if (t < j1) {
 #pragma unroll
-        for (int i = 0; i < NL; i++) ap[i] += (int64_t)c * v.l[i];
+        for (int i = 0; i < NL; i++) ap[i] += (int64_t)cf[t] * v[t].l[i];
       } else {
 #pragma unroll
-        for (int i = 0; i < NL; i++) at[i] += (int64_t)c * v.l[i];
+        for (int i = 0; i < NL; i++) at[i] += (int64_t)cf[t] * v[t].l[i];
       }
     }
   }
-  // plain terms: |limb| < 6 x 2^28 when twisted terms follow (tools/gen_wave_prog.py check_bounds)
-  Fp r;
-#pragma unroll
-  for (int i = 0; i < NL; i++) r.l[i] = (int32_t)ap[i];
+  // Both sums fit int32 limbs (|limb| < 8 x 2^28: tools/gen_wave_prog.py check_bounds).  The twisted
+  // sum joins as xi (t0 + t1 u) = (t0 - t1) + (t0 + t1) u on its unnormalised limbs (|u_i| < 2^33 in
+  // int64), and ONE carry pass reduces: the quotient comes from the top limb alone, as in fp_red_mk
+  // (the lower limbs move the value by < 2^369, far below p), so the output is normalised and in
+  // (-p/256, p + p/256).  Round 5 normalised the twisted sum, the total and then reduced: three
+  // serial carry chains where one is enough (round 6: the assembly phase was ~39 % of a Miller stage).
+  int64_t u[NL];
   if (j2) {
-    Fp t;
+    int32_t t[NL];
 #pragma unroll
-    for (int i = 0; i < NL; i++) t.l[i] = (int32_t)at[i];
-    fp_norm(t);
-    const Fp pt = dpp_fp<DPP_SWAP>(t);
-    // xi (t0 + t1 u) = (t0 - t1) + (t0 + t1) u
+    for (int i = 0; i < NL; i++) t[i] = (int32_t)at[i];
 #pragma unroll
-    for (int i = 0; i < NL; i++) r.l[i] += t.l[i] + (h ? pt.l[i] : -pt.l[i]);
+    for (int i = 0; i < NL; i++) {
+      const int32_t pt = dpp<DPP_SWAP>(t[i]);
+      u[i] = ap[i] + (int64_t)t[i] + (int64_t)(h ? pt : -pt);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NL; i++) u[i] = ap[i];
   }
-  fp_norm(r);
-  r = fp_reduce(r);
+  const int32_t q = (int32_t)((u[NL - 1] * QINV) >> 32);
+  Fp r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    acc += u[i] - (int64_t)q * (int32_t)P_L[i];
+    r.l[i] = (int32_t)acc & MASK28;
+    acc >>= 28;
+  }
+  r.l[NL - 1] = (int32_t)(acc + u[NL - 1] - (int64_t)q * (int32_t)P_L[NL - 1]);
   const int gate = (ws[0] >> 8) & 3;
   if ((gate == 1 && !act0) || (gate == 2 && !act1)) r = ((ws[0] >> 10) & 1) ? h_one() : h_zero();
   st_own(sm, ws[0] & 0xFF, h, r);
@@ -282,8 +327,8 @@ HP_D Fp shfl_fp(const Fp& a, int src_lane) {
   for (int i = 0; i < NL; i++) r.l[i] = __builtin_amdgcn_ds_bpermute(src_lane << 2, a.l[i]);
   return r;
 }
-// reduce(3 t + k a) for k = +-2 chosen at run time (fp_red_mk's one-pass reduction, same bounds)
-HP_D Fp fp_red_3k(const Fp& t, const Fp& a, int k) {
+// the round-5 form (A/B): the same quotient, then a carry chain (normalised output)
+HP_D Fp fp_red_mk_k(const Fp& t, const Fp& a, int k) {
   const int64_t top = (int64_t)t.l[NL - 1] * 3 + (int64_t)k * a.l[NL - 1];
   const int32_t q = (int32_t)((top * QINV) >> 32);
   Fp r;
@@ -297,6 +342,24 @@ HP_D Fp fp_red_3k(const Fp& t, const Fp& a, int k) {
   r.l[NL - 1] = (int32_t)(acc + top - (int64_t)q * (int32_t)P_L[NL - 1]);
   return r;
 }
+// reduce(3 t + k a) for k = +-2 chosen at run time: fp_red_mk's quotient from the top limb, then one
+// parallel carry step (fp_carry1's) instead of a carry chain: limbs in [-32, 2^28 + 32), value as
+// fp_red_mk's -- a squaring input again (cyc_run normalises once, when the run stores its result)
+HP_D Fp fp_red_3k(const Fp& t, const Fp& a, int k) {
+  if (!WV_PAR_CARRY) return fp_red_mk_k(t, a, k);
+  const int64_t top = (int64_t)t.l[NL - 1] * 3 + (int64_t)k * a.l[NL - 1];
+  const int32_t q = (int32_t)((top * QINV) >> 32);
+  int64_t v[NL];
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) v[i] = (int64_t)t.l[i] * 3 + (int64_t)k * a.l[i] - (int64_t)q * (int32_t)P_L[i];
+  v[NL - 1] = top - (int64_t)q * (int32_t)P_L[NL - 1];
+  Fp r;
+  r.l[0] = (int32_t)v[0] & MASK28;
+#pragma unroll
+  for (int i = 1; i < NL - 1; i++) r.l[i] = ((int32_t)v[i] & MASK28) + (int32_t)(v[i - 1] >> 28);
+  r.l[NL - 1] = (int32_t)(v[NL - 1] + (v[NL - 2] >> 28));
+  return r;
+}
 // position of the value a holder lane keeps: role 0 holds (f0, f3), role 1 (f1, f4), role 2 (f2, f5)
 HP_D int cyc_pos(int role, int j) { return role + 3 * j; }
 
@@ -306,11 +369,13 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
   // lane = 16 row + 4 j + 2 rr + h: squaring j of the row, component h (rr: idle copy)
   const int h = lane & 1, rr = (lane >> 1) & 1, row = lane >> 4, j = (lane >> 2) & 3;
   const bool holder = row < 3 && j < 2;
-  int count = (int)((w1 >> 48) & 0xFF);
+  // the run's count and conjugation flag are the same on every lane: read them into scalar registers
+  // so the squaring loop is a scalar loop (no per-iteration exec-mask bookkeeping)
+  int count = __builtin_amdgcn_readfirstlane((int)((w1 >> 48) & 0xFF));
 #ifdef WV_CYC_REPEAT  // timing-only A/B builds (wrong verdicts): each run squares WV_CYC_REPEAT x as often
   count *= WV_CYC_REPEAT;
 #endif
-  const bool conj = ((w1 >> 56) & 1) != 0;
+  const bool conj = (__builtin_amdgcn_readfirstlane((int)(w1 >> 56)) & 1) != 0;
   int role = row < 3 ? row : 0;
   Fp v = fp_zero();
   if (holder) v = ld_own(sm, (int)((w0 >> (8 * cyc_pos(role, j))) & 0xFF), h);
@@ -319,7 +384,9 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
 #pragma unroll 1
   for (int it = 0; it < count; it++) {
     const Fp A = shfl_fp(v, base), B = shfl_fp(v, base + 4);
-    const Fp x = j == 2 ? fp_add(A, B) : v;
+    Fp x = fp_addl(A, B);
+    fp_carry1(x);
+    x = fp_sel(j == 2, x, v);
     const Fp sq = wv_sqr(x);
     const Fp sA = shfl_fp(sq, base), sB = shfl_fp(sq, base + 4), sAB = shfl_fp(sq, base + 8);
     const Fp L = shfl_fp(v, partner);
@@ -333,6 +400,7 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
     v = r;
     if (row == 1 || row == 2) role = 3 - role;  // (f1, f4) <-> (f2, f5)
   }
+  fp_norm(v);  // the run's values are almost normalised (fp_red_3k); slots hold normalised limbs
   if (holder && rr == 0) st_own(sm, (int)((w1 >> (8 * cyc_pos(role, j))) & 0xFF), h, v);
 }
 
@@ -369,8 +437,18 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
   const uint4* hdr = (const uint4*)WV_PROG::WP_HDR;
   // descriptors are fetched one stage ahead: their L2 latency hides behind the current stage
   StageDesc cur = load_stage(hdr, off, pair);
+#ifdef WV_STAGE_CLOCK  // timing-only builds: core cycles per stage kind (M1 M2 SQ NONE INV CYC), block 0
+  uint64_t clk[6] = {0, 0, 0, 0, 0, 0};
+  int cnt[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t ph[4] = {0, 0, 0, 0};  // M1/M2/SQ stages: product, first barrier, assembly, second barrier
+  uint64_t tp1 = 0, tp2 = 0, tp3 = 0;
+  const uint64_t t_all = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll 1
   for (int st = off; st < off + nst; st++) {
+#ifdef WV_STAGE_CLOCK
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
     const StageDesc nxt = load_stage(hdr, st + 1 < off + nst ? st + 1 : st, pair);
     const uint4 hd = cur.hd;
     const uint32_t fl = hd.x;
@@ -394,7 +472,7 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
     } else if (special == 1) {
       if (pair == 0) {
         const Fp v = ld_own(sm, hd.w & 0xFF, h);
-        st_own(sm, (hd.w >> 8) & 0xFF, h, fp_reduce(h_inv_vartime(v)));
+        st_own(sm, (hd.w >> 8) & 0xFF, h, fp_reduce(h_inv_vartime<true>(v)));  // pair 0 only: uniform
       }
     } else if (kind != 3 && pair < npairs) {
       Fp r;
@@ -409,7 +487,13 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
       }
       st_own(sm, WV_PROG::WP_PROD + pair, h, r);
     }
+#ifdef WV_STAGE_CLOCK
+    tp1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#ifdef WV_STAGE_CLOCK
+    tp2 = __builtin_amdgcn_s_memtime();
+#endif
     if (pair < nouts) assemble(sm, h, cur.ad, j1, j2, act0, act1);
     if (tslot >= 0) {
       int32_t w[4 * WV_LINE_Q4];
@@ -428,9 +512,36 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
         st_own(sm, tslot + c, h, v);
       }
     }
+#ifdef WV_STAGE_CLOCK
+    tp3 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#ifdef WV_STAGE_CLOCK
+    {
+      const int sp = (cur.hd.x >> 12) & 0xF, cat = sp == 2 ? 5 : sp == 1 ? 4 : (int)(cur.hd.x & 3);
+      const uint64_t t4 = __builtin_amdgcn_s_memtime();
+      clk[cat] += t4 - t0;
+      cnt[cat]++;
+      if (cat < 3) {
+        ph[0] += tp1 - t0;
+        ph[1] += tp2 - tp1;
+        ph[2] += tp3 - tp2;
+        ph[3] += t4 - tp3;
+      }
+    }
+#endif
     cur = nxt;
   }
+#ifdef WV_STAGE_CLOCK
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    printf("STAGECLK threads %d off %d nst %d total %lu | M1 %d %lu | M2 %d %lu | SQ %d %lu | NONE %d %lu | INV %d %lu | CYC %d %lu\n",
+           (int)WV_THREADS, off, nst, (unsigned long)(__builtin_amdgcn_s_memtime() - t_all), cnt[0], (unsigned long)clk[0],
+           cnt[1], (unsigned long)clk[1], cnt[2], (unsigned long)clk[2], cnt[3], (unsigned long)clk[3], cnt[4],
+           (unsigned long)clk[4], cnt[5], (unsigned long)clk[5]);
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0)
+    printf("PHASES wave %d product %lu barrier1 %lu assembly %lu barrier2 %lu\n", (int)(threadIdx.x >> 6),
+           (unsigned long)ph[0], (unsigned long)ph[1], (unsigned long)ph[2], (unsigned long)ph[3]);
+#endif
 }
 
 // constant slots (tools/gen_wave_prog.py CONSTS): pair k writes slot k
@@ -542,7 +653,7 @@ HP_D void wave_load12(uint32_t* sm, int h, int pair, int slot, const uint32_t* v
   if (pair < 6) st_own(sm, slot + pair, h, fp_from_words(v + 24 * pair + 12 * h));
 }
 
-__global__ void __launch_bounds__(WV_THREADS) k_wave(WaveArgs a) {
+__global__ void __launch_bounds__(WV_THREADS, WV_THREADS == 64 ? 2 : 1) k_wave(WaveArgs a) {
   extern __shared__ uint32_t sm[];
   const int i = blockIdx.x;
   if (i >= a.n) return;

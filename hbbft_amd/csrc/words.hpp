@@ -115,7 +115,10 @@ HW_HD bool words_neg_if(uint32_t* x, bool neg) {  // two's-complement negation o
 // applying the round's 2x2 update matrix to the full a, b and to the coefficients u, v (divided
 // by 2^31 mod m, Montgomery style).  ~25 rounds for a 381-bit modulus instead of ~760 multiword
 // shift / subtract steps.  Fixed round count: no data-dependent termination.
-template <int N>
+// BATCH (for callers whose lanes invert the same value, the wave kernel's one inversion): a run of
+// even divsteps is taken at once (count trailing zeros, shift, double the coefficients) -- the same
+// sequence of divsteps in ~1/3 of the iterations; divergent callers keep one divstep per iteration.
+template <int N, bool BATCH = false>
 HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* out) {
   uint32_t a[N + 1], b[N + 1], u[N + 1], v[N + 1];
 #pragma unroll
@@ -140,7 +143,36 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
     uint64_t ab = ((uint64_t)a[0] & 0x7fffffffu) | (words_bits64<N>(a, n - 33) << 31);
     uint64_t bb = ((uint64_t)b[0] & 0x7fffffffu) | (words_bits64<N>(b, n - 33) << 31);
     int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
-    for (int j = 0; j < 31; j++) {
+    if (BATCH) {
+      int j = 0;
+      while (true) {
+        const int tz = ab ? __builtin_ctzll(ab) : 64;
+        const int z = tz < 31 - j ? tz : 31 - j;  // even divsteps
+        ab >>= z;
+        f1 <<= z;
+        g1 <<= z;
+        j += z;
+        if (j >= 31) break;
+        if (ab < bb) {  // odd divstep
+          const uint64_t t = ab;
+          ab = bb;
+          bb = t;
+          int64_t q = f0;
+          f0 = f1;
+          f1 = q;
+          q = g0;
+          g0 = g1;
+          g1 = q;
+        }
+        ab = (ab - bb) >> 1;
+        f0 -= f1;
+        g0 -= g1;
+        f1 *= 2;
+        g1 *= 2;
+        if (++j >= 31) break;
+      }
+    }
+    for (int j = 0; j < (BATCH ? 0 : 31); j++) {
       if (ab & 1) {
         if (ab < bb) {
           const uint64_t t = ab;
