@@ -108,6 +108,31 @@ HW_HD bool words_neg_if(uint32_t* x, bool neg) {  // two's-complement negation o
   return true;
 }
 
+// out = (x fx + y fy + q mod) / 2^31 for signed (N+1)-word x, y (two's complement, top word signed),
+// |fx|, |fy| <= 2^31, q in [0, 2^31) chosen (minv = -mod^-1 mod 2^32) so the sum is divisible by 2^31;
+// out has N+1 words, signed (the caller keeps |out| < 2^(32N+31))
+template <int N>
+HW_HD void words_lin_mont31(const uint32_t* x, int64_t fx, const uint32_t* y, int64_t fy, const uint32_t* mod,
+                            uint32_t minv, uint32_t* out) {
+  const uint32_t t0 = (uint32_t)((uint64_t)x[0] * (uint64_t)fx + (uint64_t)y[0] * (uint64_t)fy);
+  const uint64_t q = (uint64_t)((t0 * minv) & 0x7fffffffu);
+  uint32_t t[N + 2];
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i <= N; i++) {
+    const int64_t xi = i < N ? (int64_t)x[i] : (int64_t)(int32_t)x[N];
+    const int64_t yi = i < N ? (int64_t)y[i] : (int64_t)(int32_t)y[N];
+    const int64_t p1 = xi * fx, p2 = yi * fy;
+    const uint64_t p3 = i < N ? q * mod[i] : 0;
+    const int64_t sw = (int64_t)(uint32_t)p1 + (int64_t)(uint32_t)p2 + (int64_t)(uint32_t)p3 + c;
+    t[i] = (uint32_t)sw;
+    c = (sw >> 32) + (p1 >> 32) + (p2 >> 32) + (int64_t)(p3 >> 32);
+  }
+  t[N + 1] = (uint32_t)c;
+#pragma unroll
+  for (int i = 0; i <= N; i++) out[i] = (t[i] >> 31) | (t[i + 1] << 1);
+}
+
 // out = a^-1 mod `mod` (odd modulus of at most 32N - 2 bits, a canonical); 0 when a is 0 or not
 // invertible.  Variable time, for public values only.  T. Pornin's optimized binary GCD
 // (eprint 2020/972, Algorithm 2): the binary GCD's 2 len(m) - 1 divsteps in rounds of 31, each round
@@ -136,9 +161,17 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
   const uint32_t minv = 0u - inv;
   const int rounds = (2 * words_bitlen<N>(mod) - 1 + 30) / 31;
   for (int r = 0; r < rounds; r++) {
-    int n = words_bitlen<N>(a);
-    const int nb = words_bitlen<N>(b);
-    if (nb > n) n = nb;
+    int n;
+    if (BATCH) {  // max(len a, len b) = len(a | b)
+      uint32_t o[N];
+#pragma unroll
+      for (int i = 0; i < N; i++) o[i] = a[i] | b[i];
+      n = words_bitlen<N>(o);
+    } else {
+      n = words_bitlen<N>(a);
+      const int nb = words_bitlen<N>(b);
+      if (nb > n) n = nb;
+    }
     if (n < 64) n = 64;
     uint64_t ab = ((uint64_t)a[0] & 0x7fffffffu) | (words_bits64<N>(a, n - 33) << 31);
     uint64_t bb = ((uint64_t)b[0] & 0x7fffffffu) | (words_bits64<N>(b, n - 33) << 31);
@@ -210,6 +243,20 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
       a[i] = na[i];
       b[i] = nbw[i];
     }
+    if (BATCH) {
+      // (u, v) <- ((u f0 + v g0) / 2^31, (u f1 + v g1) / 2^31), signed and NOT reduced mod m: with
+      // |f0| + |g0| <= 2^31 (and the same for f1, g1) each round adds at most m to the bound, so
+      // |u|, |v| < 26 m < 2^386 after the 25 rounds of a 381-bit modulus; one reduction at the end
+      uint32_t nu0[N + 1], nv0[N + 1];
+      words_lin_mont31<N>(u, f0, v, g0, mod, minv, nu0);
+      words_lin_mont31<N>(u, f1, v, g1, mod, minv, nv0);
+#pragma unroll
+      for (int i = 0; i <= N; i++) {
+        u[i] = nu0[i];
+        v[i] = nv0[i];
+      }
+      continue;
+    }
     // (u, v) <- ((u f0 + v g0) / 2^31, (u f1 + v g1) / 2^31) mod m
     uint32_t nu[2][N + 1];
 #pragma unroll
@@ -269,6 +316,16 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
     }
   }
   bool one = b[N] == 0 && words_is_one<N>(b);
+  if (BATCH && one) {  // v signed, |v| < 26 m: into [0, m)
+    while ((int32_t)v[N] < 0) {
+      const uint32_t c = words_add<N>(v, mod);
+      v[N] += c;
+    }
+    while (v[N] != 0 || words_geq<N>(v, mod)) {
+      const uint32_t br = words_sub<N>(v, mod);
+      v[N] -= br;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < N; i++) out[i] = one ? v[i] : 0u;
 }
