@@ -404,6 +404,13 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
   if (holder && rr == 0) st_own(sm, (int)((w1 >> (8 * cyc_pos(role, j))) & 0xFF), h, v);
 }
 
+// the final exponentiation's one inversion (pair 0; both lanes invert the same norm, so the batched
+// variable-time form; k_wave64 also keeps its coefficients unreduced, words.hpp INV_LAZY, which makes
+// the 256-register k_wave spill -- round 6 A/B, profiles/r06/ab_inv.txt)
+HP_D Fp wv_inv(const Fp& v) {
+  return fp_reduce(h_inv_vartime<WV_THREADS == 128 ? (hb::INV_BATCH | hb::INV_LAZY) : hb::INV_BATCH>(v));
+}
+
 // this lane's descriptors of one stage (product: K u64 of its pair; assembly: 8 u16 of its output)
 struct StageDesc {
   uint4 hd;
@@ -472,7 +479,7 @@ HP_D void run_stages(uint32_t* sm, int off, int nst, int h, int pair, bool act0,
     } else if (special == 1) {
       if (pair == 0) {
         const Fp v = ld_own(sm, hd.w & 0xFF, h);
-        st_own(sm, (hd.w >> 8) & 0xFF, h, fp_reduce(h_inv_vartime<true>(v)));  // pair 0 only: uniform
+        st_own(sm, (hd.w >> 8) & 0xFF, h, wv_inv(v));  // pair 0 only: uniform
       }
     } else if (kind != 3 && pair < npairs) {
       Fp r;

@@ -138,7 +138,7 @@ HP_D bool lp_both(bool v) { return (v ? 1 : 0) & dpp<DPP_SWAP>(v ? 1 : 0); }
 HP_D bool h_is_zero(const Fp& a) { return lp_both(fp_is_zero(a)); }
 // 1 / a in Fp2 with a variable-time inverse of the (public) norm: both lanes invert the same norm.
 // a = 0 gives 0 (the binary Euclid loop would not terminate on a zero norm).
-template <bool BATCH = false>
+template <int MODE = 0>
 HP_D Fp h_inv_vartime(const Fp& a) {
   const Fp s = fp_sqr(a);
   const Fp n = fp_add(s, dpp_fp<DPP_SWAP>(s));
@@ -151,7 +151,7 @@ HP_D Fp h_inv_vartime(const Fp& a) {
 #pragma unroll
   for (int i = 0; i < 12; i++) p[i] = hb::PM2_W[i];
   p[0] += 2;  // p - 2 + 2
-  hb::words_inv_vartime<12, BATCH>(w, p, r);
+  hb::words_inv_vartime<12, MODE>(w, p, r);
   return h_conj(fp_mul(a, fp_from_words(r)));
 }
 

@@ -140,11 +140,16 @@ HW_HD void words_lin_mont31(const uint32_t* x, int64_t fx, const uint32_t* y, in
 // applying the round's 2x2 update matrix to the full a, b and to the coefficients u, v (divided
 // by 2^31 mod m, Montgomery style).  ~25 rounds for a 381-bit modulus instead of ~760 multiword
 // shift / subtract steps.  Fixed round count: no data-dependent termination.
-// BATCH (for callers whose lanes invert the same value, the wave kernel's one inversion): a run of
-// even divsteps is taken at once (count trailing zeros, shift, double the coefficients) -- the same
-// sequence of divsteps in ~1/3 of the iterations; divergent callers keep one divstep per iteration.
-template <int N, bool BATCH = false>
+// MODE (for callers whose lanes invert the same value, the wave kernels' one inversion; divergent
+// callers keep 0): bit 0 (INV_BATCH) takes a run of even divsteps at once (count trailing zeros,
+// shift, double the coefficients) -- the same divsteps in ~1/3 of the loop iterations; bit 1
+// (INV_LAZY) takes the bit length of a | b once and keeps the coefficients u, v signed and unreduced across the
+// rounds (one reduction at the end) -- fewer instructions, but more live registers: the two-wave
+// k_wave64 takes it, the 256-register k_wave does not (it spills there).
+constexpr int INV_BATCH = 1, INV_LAZY = 2;
+template <int N, int MODE = 0>
 HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* out) {
+  constexpr bool BATCH = (MODE & INV_BATCH) != 0, LAZY = (MODE & INV_LAZY) != 0;
   uint32_t a[N + 1], b[N + 1], u[N + 1], v[N + 1];
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -162,7 +167,7 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
   const int rounds = (2 * words_bitlen<N>(mod) - 1 + 30) / 31;
   for (int r = 0; r < rounds; r++) {
     int n;
-    if (BATCH) {  // max(len a, len b) = len(a | b)
+    if (LAZY) {  // max(len a, len b) = len(a | b) (in k_wave this form measured slower: kept to k_wave64)
       uint32_t o[N];
 #pragma unroll
       for (int i = 0; i < N; i++) o[i] = a[i] | b[i];
@@ -243,7 +248,7 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
       a[i] = na[i];
       b[i] = nbw[i];
     }
-    if (BATCH) {
+    if (LAZY) {
       // (u, v) <- ((u f0 + v g0) / 2^31, (u f1 + v g1) / 2^31), signed and NOT reduced mod m: with
       // |f0| + |g0| <= 2^31 (and the same for f1, g1) each round adds at most m to the bound, so
       // |u|, |v| < 26 m < 2^386 after the 25 rounds of a 381-bit modulus; one reduction at the end
@@ -316,7 +321,7 @@ HW_HD void words_inv_vartime(const uint32_t* y, const uint32_t* mod, uint32_t* o
     }
   }
   bool one = b[N] == 0 && words_is_one<N>(b);
-  if (BATCH && one) {  // v signed, |v| < 26 m: into [0, m)
+  if (LAZY && one) {  // v signed, |v| < 26 m: into [0, m)
     while ((int32_t)v[N] < 0) {
       const uint32_t c = words_add<N>(v, mod);
       v[N] += c;

@@ -1,6 +1,6 @@
-// CPU check of hbbft_amd/csrc/words.hpp's variable-time inverse: the batched form (runs of even
-// divsteps at once, lazily reduced coefficients -- the wave kernel's one inversion) against the
-// per-divstep form, and both against y * y^-1 == 1, for the BLS12-381 base field (12 words) and scalar
+// CPU check of hbbft_amd/csrc/words.hpp's variable-time inverse: every MODE (runs of even divsteps
+// at once, lazily reduced coefficients -- the wave kernels' one inversion) against the per-divstep
+// form, and both against y * y^-1 == 1, for the BLS12-381 base field (12 words) and scalar
 // field (8 words).  Built and run by tests/test_words_inv.py.
 #include <cstdint>
 #include <cstdio>
@@ -52,12 +52,14 @@ static int run(const uint32_t* m, uint32_t topmask, int iters, uint64_t seed) {
       for (int i = 0; i < N; i++) y[i] = m[i];
       y[0] -= 1;  // m - 1
     }
-    uint32_t r0[N], r1[N];
-    hb::words_inv_vartime<N, false>(y, m, r0);
-    hb::words_inv_vartime<N, true>(y, m, r1);
+    uint32_t r0[N], r1[N], r2[N], r3[N];
+    hb::words_inv_vartime<N, 0>(y, m, r0);
+    hb::words_inv_vartime<N, hb::INV_BATCH>(y, m, r1);
+    hb::words_inv_vartime<N, hb::INV_LAZY>(y, m, r2);
+    hb::words_inv_vartime<N, hb::INV_BATCH | hb::INV_LAZY>(y, m, r3);
     bool same = true, zero = true;
     for (int i = 0; i < N; i++) {
-      same = same && r0[i] == r1[i];
+      same = same && r0[i] == r1[i] && r0[i] == r2[i] && r0[i] == r3[i];
       zero = zero && y[i] == 0;
     }
     const bool ok = same && (zero || (it < 200 ? mul_is_one<N>(y, r1, m) : true));
