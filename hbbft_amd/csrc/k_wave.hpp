@@ -68,14 +68,7 @@ HP_D void st_own(uint32_t* sm, int slot, int h, const Fp& a) {
 // (taken from limb i - 1's value BEFORE this step).  For |limb| < 2^31 the result has limbs in
 // [-8, 2^28 + 8) and the same value -- "almost normalised", which is all the product bounds need
 // (sfp.hpp (M): |limb| <= 2^29), at the latency of one step instead of fp_norm's 13 dependent ones.
-#ifndef WV_PAR_CARRY
-#define WV_PAR_CARRY 1
-#endif
 HP_D void fp_carry1(Fp& a) {
-  if (!WV_PAR_CARRY) {  // A/B: the sequential carry chain
-    fp_norm(a);
-    return;
-  }
   int32_t c[NL];
 #pragma unroll
   for (int i = 0; i < NL - 1; i++) c[i] = a.l[i] >> 28;
@@ -327,26 +320,10 @@ HP_D Fp shfl_fp(const Fp& a, int src_lane) {
   for (int i = 0; i < NL; i++) r.l[i] = __builtin_amdgcn_ds_bpermute(src_lane << 2, a.l[i]);
   return r;
 }
-// the round-5 form (A/B): the same quotient, then a carry chain (normalised output)
-HP_D Fp fp_red_mk_k(const Fp& t, const Fp& a, int k) {
-  const int64_t top = (int64_t)t.l[NL - 1] * 3 + (int64_t)k * a.l[NL - 1];
-  const int32_t q = (int32_t)((top * QINV) >> 32);
-  Fp r;
-  int64_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < NL - 1; i++) {
-    acc += (int64_t)t.l[i] * 3 + (int64_t)k * a.l[i] - (int64_t)q * (int32_t)P_L[i];
-    r.l[i] = (int32_t)acc & MASK28;
-    acc >>= 28;
-  }
-  r.l[NL - 1] = (int32_t)(acc + top - (int64_t)q * (int32_t)P_L[NL - 1]);
-  return r;
-}
 // reduce(3 t + k a) for k = +-2 chosen at run time: fp_red_mk's quotient from the top limb, then one
 // parallel carry step (fp_carry1's) instead of a carry chain: limbs in [-32, 2^28 + 32), value as
 // fp_red_mk's -- a squaring input again (cyc_run normalises once, when the run stores its result)
 HP_D Fp fp_red_3k(const Fp& t, const Fp& a, int k) {
-  if (!WV_PAR_CARRY) return fp_red_mk_k(t, a, k);
   const int64_t top = (int64_t)t.l[NL - 1] * 3 + (int64_t)k * a.l[NL - 1];
   const int32_t q = (int32_t)((top * QINV) >> 32);
   int64_t v[NL];
@@ -371,10 +348,7 @@ HP_D void cyc_run(uint32_t* sm, int lane, uint64_t w0, uint64_t w1) {
   const bool holder = row < 3 && j < 2;
   // the run's count and conjugation flag are the same on every lane: read them into scalar registers
   // so the squaring loop is a scalar loop (no per-iteration exec-mask bookkeeping)
-  int count = __builtin_amdgcn_readfirstlane((int)((w1 >> 48) & 0xFF));
-#ifdef WV_CYC_REPEAT  // timing-only A/B builds (wrong verdicts): each run squares WV_CYC_REPEAT x as often
-  count *= WV_CYC_REPEAT;
-#endif
+  const int count = __builtin_amdgcn_readfirstlane((int)((w1 >> 48) & 0xFF));
   const bool conj = (__builtin_amdgcn_readfirstlane((int)(w1 >> 56)) & 1) != 0;
   int role = row < 3 ? row : 0;
   Fp v = fp_zero();
@@ -728,9 +702,7 @@ __global__ void __launch_bounds__(WV_THREADS, WV_THREADS == 64 ? 2 : 1) k_wave(W
         fp_to_words(ld_own(sm, WV_PROG::WP_F + pair, h), a.value_out + (size_t)i * 144 + 24 * pair + 12 * h);
       return;
     }
-#ifndef WV_FE_SKIP  // timing-only A/B builds (wrong verdicts): Miller loop without the final exponentiation
     run_stages(sm, WV_PROG::WP_FE_OFF, WV_PROG::WP_FE_N, h, pair, act0, act1, tl0, tl1);
-#endif
   }
   // e = f^(3 (p^12 - 1) / r) in slots E0..E5 (w-basis)
   bool ok = true;
