@@ -50,6 +50,36 @@ def test_g2_criterion_equals_r_mul():
         assert want == (label == "subgroup"), label
 
 
+def g2_criterion_on_isomorph(pt):
+    """The decoder's two-role form (k_g2_decompress, session 2 of round 6): with rhs = x^3 + b = y^2
+    the isomorphism iota(X, Y) = (y^2 X, y^3 Y) sends P to P' = (rhs x, rhs^2) -- known from x alone, so
+    [|x|] P' runs beside the square root -- and psi(P) to (C1 rhs conj(x), C2 rhs N(y)), N(y) = y conj(y)
+    in Fp (the same for both roots).  iota commutes with [k] (the a = 0 formulas never read b), so
+    psi(P) == -[|x|] P  <=>  [|x|] P' == (C1 rhs conj(x), -C2 rhs N(y))."""
+    if pt is None:
+        return True
+    x, y = pt
+    rhs = C.f2_add(C.f2_mul(C.f2_sqr(x), x), C.B2)
+    assert not C.f2_is_zero(rhs)  # #E'(Fp2) = h2 r is odd: no point has y = 0
+    Pp = (C.f2_mul(rhs, x), C.f2_sqr(rhs))
+    J = (C.F2_ONE, C.F2_ONE, C.F2_ZERO)
+    for bit in bin(C.X_ABS)[2:]:
+        J = C._j2_dbl(J)
+        if bit == "1":
+            J = C._j2_add_aff(J, Pp)
+    norm = (y[0] * y[0] + y[1] * y[1]) % C.P
+    want = (C.f2_mul(C.f2_mul(rhs, C.f2_conj(x)), PSI_C1), C.f2_neg(C.f2_muls(C.f2_mul(rhs, PSI_C2), norm)))
+    return C._j2_to_aff(J) == want
+
+
+def test_g2_criterion_on_isomorph_equals_r_mul():
+    for label, pt in S.sample(True, 12, seed=603):
+        want = C.g2_mul(pt, C.R) is None
+        assert g2_criterion_on_isomorph(pt) == want, label
+        neg = C.g2_neg(pt)
+        assert g2_criterion_on_isomorph(neg) == want, label
+
+
 def test_criteria_determinants():
     """Why the criteria are exact on the whole curve: on the l-power torsion (l != r) the map
     phi + [x^2] has determinant N(-x^2 - phi) = x^4 - x^2 + 1 = r (phi^2 + phi + 1 = 0), and
