@@ -6,6 +6,8 @@
 // the byte-level flag checks and the big-endian -> little-endian word reversal (wire.hpp).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "curve.hpp"
 #include "wire.hpp"
 #include "sqrt_chain.inc"
@@ -75,16 +77,6 @@ __device__ __forceinline__ bool jac_eq_affine(const Jac<F>& q, const F& x, const
 __device__ __forceinline__ bool g1_in_subgroup(const Fp& x, const Fp& y) {
   const Jac<Fp> q = mul_absx_jac(mul_absx_affine(x, y));
   return jac_eq_affine(q, fp_mul(x, fp_const(BETA_M)), fp_neg(y));
-}
-
-// [x] P == psi(P)  <=>  [|x|] P == -psi(P);  psi(x) = conj(x) * (c1 u) = (x1 c1) + (x0 c1) u,
-// psi(y) = conj(y) * c2
-__device__ __forceinline__ bool g2_in_subgroup(const Fp2& x, const Fp2& y) {
-  const Jac<Fp2> q = mul_absx_affine(x, y);
-  const Fp c1 = fp_const(PSI_C1_C1);
-  const Fp2 px = {fp_mul(x.c1, c1), fp_mul(x.c0, c1)};
-  const Fp2 py = f2_mul(f2_conj(y), Fp2{fp_const(PSI_C2_C0), fp_const(PSI_C2_C1)});
-  return jac_eq_affine(q, px, f2_neg(py));
 }
 
 // ---------------------------------------------------------------------------- decompression
@@ -191,41 +183,88 @@ __device__ __forceinline__ bool f2_sqrt_norm(const Fp2& a, Fp2& out) {
   return f2_is_zero(f2_sub(f2_sqr(y), a));
 }
 
-__global__ void __launch_bounds__(256) k_g2_decompress(int n, const uint32_t* __restrict__ xw,
+// G2: two waves per 64 points, as G1.  The subgroup test needs y only through its norm: with
+// rhs = x^3 + b = y^2, iota(X, Y) = (y^2 X, y^3 Y) maps E' isomorphically onto Y^2 = X^3 + b rhs^3 and
+// sends P to P' = (rhs x, rhs^2) -- known from x alone -- and psi(P) = (C1 conj(x), C2 conj(y)) to
+// (C1 rhs conj(x), C2 rhs N(y)) with N(y) = y conj(y) in Fp (the same for both roots).  iota commutes
+// with [k] and the a = 0 formulas never read b, so psi(P) == -[|x|] P  <=>  [|x|] P' == (C1 rhs conj(x),
+// -C2 rhs N(y)) (tests/test_subgroup_criteria.py checks the equivalence on every cofactor torsion).
+// Wave 1 runs [|x|] P' (68 group operations over Fp2) while wave 0 takes the square root (two
+// (p - 3) / 4 chains); wave 0 then publishes N(y) through LDS and wave 1 finishes the comparison.
+// #E'(Fp2) = h2 r is odd, so no point has rhs = 0 (where iota would degenerate).
+template <int WPS>
+__global__ void __launch_bounds__(128, WPS) k_g2_decompress(int n, const uint32_t* __restrict__ xw,
                                                        const uint8_t* __restrict__ flags, uint32_t* __restrict__ out,
                                                        uint8_t* __restrict__ ok) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t* o = out + (size_t)i * G2_WORDS;
-  const uint8_t f = flags[i];
-  bool valid = false;
-  uint32_t x[24], y[24];
-  for (int k = 0; k < 24; k++) x[k] = xw[(size_t)i * 24 + k], y[k] = 0;
-  if (f & hbl::WIRE_INFINITY) {
-    valid = true;
-    for (int k = 0; k < 24; k++) x[k] = 0;
-  } else if (!(f & hbl::WIRE_REJECT)) {
-    uint32_t p[12];
+  __shared__ uint32_t nrm[NL * 64];
+  __shared__ uint8_t in_group[64];
+  const int lane = threadIdx.x & 63, role = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const bool live = i < n;
+  const uint8_t f = live ? flags[i] : hbl::WIRE_REJECT;
+  const uint32_t* xi = xw + (size_t)(live ? i : 0) * 24;
+  uint32_t* o = out + (size_t)(live ? i : 0) * G2_WORDS;
+  bool try_point;
+  {
+    uint32_t x[24], p[12];
+    for (int k = 0; k < 24; k++) x[k] = xi[k];
     for (int k = 0; k < 12; k++) p[k] = PM2_W[k];
     p[0] += 2;
-    if (words_gt(p, x, 12) && words_gt(p, x + 12, 12)) {
-      const Fp2 xm = {fp_from_words(x), fp_from_words(x + 12)};
-      const Fp2 b2 = {fp_const(B1_M), fp_const(B1_M)};  // 4 (1 + u)
-      const Fp2 rhs = f2_add(f2_mul(f2_sqr(xm), xm), b2);
-      Fp2 ym;
-      if (f2_sqrt_norm(rhs, ym)) {
-        const Fp2 ny = f2_neg(ym);
-        if (f2_gt_canon(ym, ny) != ((f & hbl::WIRE_GREATEST) != 0)) ym = ny;
-        fp_to_words(ym.c0, y);
-        fp_to_words(ym.c1, y + 12);
-        valid = g2_in_subgroup(xm, ym);
-      }
+    try_point = !(f & hbl::WIRE_INFINITY) && !(f & hbl::WIRE_REJECT) && words_gt(p, x, 12) && words_gt(p, x + 12, 12);
+  }
+  const Fp2 b2 = {fp_const(B1_M), fp_const(B1_M)};  // 4 (1 + u)
+  bool valid = false, gx = false;
+  Fp2 qy, w;  // wave 1 only, across the barrier: [|x|] P' .y and the Y target before its factor N(y)
+  if (role == 1) {
+    if (try_point) {
+      Fp2 xm = {fp_from_words(xi), fp_from_words(xi + 12)};
+      Fp2 rhs = f2_add(f2_mul(f2_sqr(xm), xm), b2);
+      const Jac<Fp2> q = mul_absx_affine(f2_mul(rhs, xm), f2_sqr(rhs));
+      xm = {fp_from_words(xi), fp_from_words(xi + 12)};  // reloaded: not live across the chain
+      rhs = f2_add(f2_mul(f2_sqr(xm), xm), b2);
+      // target iota(-psi(P)) = (C1 rhs conj(x), -C2 rhs N(y)); C1 = c1 u, so C1 conj(x) = (x1 c1, x0 c1)
+      const Fp c1 = fp_const(PSI_C1_C1);
+      const Fp2 tx = f2_mul(rhs, Fp2{fp_mul(xm.c1, c1), fp_mul(xm.c0, c1)});
+      const Fp2 z2 = f2_sqr(q.z);
+      gx = !jac_is_zero(q) && f2_is_zero(f2_sub(q.x, f2_mul(tx, z2)));
+      w = f2_neg(f2_mul(f2_mul(rhs, Fp2{fp_const(PSI_C2_C0), fp_const(PSI_C2_C1)}), f2_mul(z2, q.z)));
+      qy = q.y;
+    }
+  } else if (f & hbl::WIRE_INFINITY) {
+    valid = live;  // the point at infinity (all-zero ABI words)
+    if (live)
+      for (int k = 0; k < G2_WORDS; k++) o[k] = 0u;
+  } else if (try_point) {
+    const Fp2 xm = {fp_from_words(xi), fp_from_words(xi + 12)};
+    const Fp2 rhs = f2_add(f2_mul(f2_sqr(xm), xm), b2);
+    Fp2 ym;
+    if (f2_sqrt_norm(rhs, ym)) {
+      const Fp2 ny = f2_neg(ym);
+      if (f2_gt_canon(ym, ny) != ((f & hbl::WIRE_GREATEST) != 0)) ym = ny;
+      const Fp nm = fp_add(fp_sqr(ym.c0), fp_sqr(ym.c1));
+      for (int k = 0; k < NL; k++) nrm[k * 64 + lane] = nm.l[k];
+      // on the curve: written now, zeroed after the second barrier when not in the subgroup
+      for (int k = 0; k < 24; k++) o[k] = xi[k];
+      fp_to_words(ym.c0, o + 24);
+      fp_to_words(ym.c1, o + 36);
+      valid = true;
     }
   }
-  for (int k = 0; k < 24; k++) {
-    o[k] = valid ? x[k] : 0u;
-    o[24 + k] = valid ? y[k] : 0u;
+  __syncthreads();
+  if (role == 1) {
+    bool g = false;
+    if (try_point && gx) {
+      Fp nm;
+      for (int k = 0; k < NL; k++) nm.l[k] = nrm[k * 64 + lane];
+      g = f2_is_zero(f2_sub(qy, Fp2{fp_mul(w.c0, nm), fp_mul(w.c1, nm)}));
+    }
+    in_group[lane] = g ? 1 : 0;
   }
+  __syncthreads();
+  if (role == 1 || !live) return;
+  if (try_point) valid = valid && in_group[lane] != 0;
+  if (!valid)
+    for (int k = 0; k < G2_WORDS; k++) o[k] = 0u;
   ok[i] = valid ? 1 : 0;
 }
 
@@ -282,8 +321,17 @@ hipError_t g1_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t
 
 hipError_t g2_decompress(hipStream_t s, int n, const uint32_t* xw, const uint8_t* flags, void* out, uint8_t* ok) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(hb::k_g2_decompress, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, xw, flags,
-                     (uint32_t*)out, ok);
+  // one wave per SIMD: 512 registers, no spills; two: 256 registers (spills) and twice the waves in flight
+  static const int waves = [] {
+    const char* v = std::getenv("HBH_G2_DEC_WAVES");
+    return v ? std::atoi(v) : 2;
+  }();
+  if (waves == 1)
+    hipLaunchKernelGGL(hb::k_g2_decompress<1>, dim3((unsigned)((n + 63) / 64)), dim3(128), 0, s, n, xw, flags,
+                       (uint32_t*)out, ok);
+  else
+    hipLaunchKernelGGL(hb::k_g2_decompress<2>, dim3((unsigned)((n + 63) / 64)), dim3(128), 0, s, n, xw, flags,
+                       (uint32_t*)out, ok);
   return hipGetLastError();
 }
 
